@@ -1,0 +1,118 @@
+// ddmi — internal declarations shared by the HIP kernel TUs and the runtime.
+// All feature maps live in HBM as fp32 NHWC ("channels-last"): a pixel's channel vector is
+// contiguous, so implicit-GEMM convs read 16-B float4 channel slices and the BEV gathers of
+// the decoder read whole 1 KB rows (see DESIGN.md §Data layout).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#define DD_HIP_CHECK(expr)                                                              \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                               " at " __FILE__ ":" + std::to_string(__LINE__) + ": " #expr); \
+  } while (0)
+
+namespace ddmi {
+
+// Strided 4-D view (n, h, w, c) with element strides; c stride is sc.
+struct View4 {
+  float* p = nullptr;
+  int64_t sn = 0, sh = 0, sw = 0, sc = 1;
+};
+
+// ----------------------------------------------------------------------------------------
+// Implicit-GEMM convolution / GEMM on fp32 MFMA (conv_gemm.hip).
+//   out[n,oh,ow,co] = act( sum_{kh,kw,ci} in[n, oh*s-p+kh, ow*s-p+kw, ci] * W(co; kh,kw,ci)
+//                          + bias[co] + res[n,oh,ow,co] )
+// GEMM view: M = Nimg*Ho*Wo, N = Cout, K = KH*KW*Cin (k order kh, kw, ci).
+// Input channel stride must be 1 and Cin % 4 == 0; in_sw/in_sh/in_sn are element strides.
+// W(co; k) = wgt[co*ldb + k] (b_kn = 0, "nn.Linear / OHWI" layout) or wgt[k*ldb + co] (b_kn = 1).
+// Batched launches (gridDim.z = batch): every pointer is offset by z1*?_z1 + z2*?_z2 with
+// z1 = z / zdiv, z2 = z % zdiv (used for per-(scene, head) attention GEMMs).
+struct ConvArgs {
+  const float* in = nullptr;
+  int64_t in_sn = 0, in_sh = 0, in_sw = 0;
+  int H = 1, W = 1, Cin = 0;
+  const float* wgt = nullptr;
+  int64_t ldb = 0;
+  int b_kn = 0;
+  const float* bias = nullptr;
+  const float* res = nullptr;
+  int64_t res_sn = 0, res_sh = 0, res_sw = 0;
+  float* out = nullptr;
+  int64_t out_sn = 0, out_sh = 0, out_sw = 0;
+  int Nimg = 1, Ho = 1, Wo = 1, Cout = 0;
+  int KH = 1, KW = 1, stride = 1, pad = 0;
+  int relu = 0;
+  float alpha = 1.0f;  // scale applied to the accumulator before bias/res
+  int batch = 1, zdiv = 1;
+  int64_t in_z1 = 0, in_z2 = 0, w_z1 = 0, w_z2 = 0, out_z1 = 0, out_z2 = 0, res_z1 = 0, res_z2 = 0;
+  int64_t flops_K = -1;  // algorithmic K per output (excluding channel padding); -1 = KH*KW*Cin
+};
+void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
+
+// ----------------------------------------------------------------------------------------
+// Bandwidth / small kernels (elementwise.hip)
+// NCHW fp32 (B, C, H, W) -> NHWC padded to Cp channels (zero fill).
+void launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int H, int W, int Cp, hipStream_t st);
+// 3x3 / stride 2 / pad 1 max pool, NHWC contiguous.
+void launch_maxpool3x3s2(const float* in, float* out, int B, int H, int W, int C, int Ho, int Wo,
+                         hipStream_t st);
+// Adaptive average pool with exact integer windows (H % oh == 0, W % ow == 0), NHWC contiguous in;
+// out (n, y, x, c) strided; optional add[y*ow + x][c] (broadcast over n).
+void launch_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow, View4 out,
+                    const float* add, hipStream_t st);
+// Bilinear resize, align_corners=False (PyTorch upsample_bilinear2d semantics):
+// out[n,y,x,c] (= or +=) bilinear(in)[n,y,x,c]. ratio_h/ratio_w = in/out unless a scale factor is given.
+void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float ratio_h,
+                     float ratio_w, int accumulate, hipStream_t st);
+// Row LayerNorm (eps 1e-5): y[r] = LN(x[r] + res[r / res_div]) * g + b, then optional FiLM
+// y = y * (1 + film_scale) + film_shift. C <= 2048. In-place allowed (y == x).
+void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldres, int res_div,
+                      const float* g, const float* b, const float* film_scale, const float* film_shift,
+                      float* y, int64_t ldy, int rows, int C, hipStream_t st);
+// Row softmax of (scale * x), in place, rows of length L (<= 1024), row stride ld.
+void launch_softmax_rows(float* x, int64_t ld, int rows, int L, float scale, hipStream_t st);
+// dst[r][:] = src[r % nsrc][:] for r < rows (row length C, contiguous).
+void launch_broadcast_rows(const float* src, int nsrc, float* dst, int rows, int C, hipStream_t st);
+// y = act(x) elementwise, n elements; act 0 = mish, 1 = relu.
+void launch_activation(const float* x, float* y, int64_t n, int act, hipStream_t st);
+
+// ----------------------------------------------------------------------------------------
+// Decoder kernels (decoder.hip)
+// img = sqrt(a)*norm_odo(anchor) + sqrt(1-a)*noise; (B, Q, P, 2)
+void launch_ddim_init(const float* anchor, const float* noise, float* img, int B, int QP, float sa,
+                      float s1a, hipStream_t st);
+// Uploads the sine-embedding frequency table (call once per device before launch_traj_embed).
+void decoder_init_constants();
+// pts = denorm_odo(clamp(img, -1, 1)); emb = gen_sineembed_for_position(pts, 64).flatten(-2)
+void launch_traj_embed(const float* img, float* pts, float* emb, int rows, int P, hipStream_t st);
+// SinusoidalPosEmb(dim) of a scalar timestep, written to out[dim].
+void launch_timestep_embed(float t, float* out, int dim, hipStream_t st);
+// GridSampleCrossBEVAttention core: per (scene, query): softmax over P logits, bilinear gather of
+// value (NHWC, Hv x Wv x C, zero padding, align_corners=False) at P points, weighted sum -> out[C].
+void launch_bev_sample_attn(const float* logits, const float* pts, const float* value, float* out,
+                            int B, int Q, int P, int Hv, int Wv, int C, float inv_max_x,
+                            float inv_max_y, hipStream_t st);
+// Small multi-head attention: out[b,i,h*hd+d] = sum_j softmax_j(q.k / sqrt(hd)) v. Lk <= 128, hd <= 64.
+void launch_mha_small(const float* q, int64_t ldq, const float* k, const float* v, int64_t ldkv,
+                      float* out, int64_t ldo, int B, int Lq, int Lk, int nh, int hd,
+                      int64_t q_bstride, int64_t kv_bstride, int64_t o_bstride, hipStream_t st);
+// reg (rows, P, 3) from the raw branch output r (rows, P*3): xy += pts, heading = tanh * pi;
+// optionally also writes the cascade's next points (rows, P, 2).
+void launch_reg_finalize(const float* r, const float* pts, float* reg, float* pts_next, int rows, int P,
+                         hipStream_t st);
+// img = DDIM.step(norm_odo(reg[..., :2]), t -> t-1, img), eta = 0, prediction 'sample', clip.
+void launch_ddim_step(const float* reg, float* img, int rows, int P, float a_t, float a_prev,
+                      hipStream_t st);
+// argmax over Q cls logits per scene, gather reg[b, argmax] -> traj (B, P, 3); also writes index.
+void launch_select_mode(const float* cls, const float* reg, float* traj, int* idx, int B, int Q, int P,
+                        hipStream_t st);
+// Agent head post-processing: states (rows, 5) in place: [0:2] = tanh*32, [2] = tanh*pi.
+void launch_agent_post(float* states, int rows, hipStream_t st);
+
+}  // namespace ddmi

@@ -1,0 +1,162 @@
+// Single-kernel C-ABI entry points (include/ddmi.h, "single-op entry points"): used by the GPU
+// parity tests to check each kernel in isolation against PyTorch-CPU fp32 on the same inputs.
+#include <cmath>
+#include <string>
+
+#include "../../include/ddmi.h"
+#include "common.h"
+
+namespace {
+thread_local std::string g_op_err;
+
+template <class F>
+int op_guard(F&& f) {
+  try {
+    f();
+    return DD_OK;
+  } catch (const std::invalid_argument& e) {
+    g_op_err = e.what();
+    return DD_ERR_INVALID;
+  } catch (const std::exception& e) {
+    g_op_err = e.what();
+    return DD_ERR_RUNTIME;
+  }
+}
+hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+}  // namespace
+
+using namespace ddmi;
+
+extern "C" {
+
+const char* dd_op_last_error(void) { return g_op_err.c_str(); }
+
+int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias, const float* res,
+                 float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {
+  return op_guard([&] {
+    ConvArgs a;
+    a.in = in;
+    a.in_sw = Cin;
+    a.in_sh = (int64_t)W * Cin;
+    a.in_sn = (int64_t)H * W * Cin;
+    a.H = H;
+    a.W = W;
+    a.Cin = Cin;
+    a.wgt = wgt;
+    a.ldb = (int64_t)KH * KW * Cin;
+    a.bias = bias;
+    a.Nimg = B;
+    a.Ho = (H + 2 * pad - KH) / stride + 1;
+    a.Wo = (W + 2 * pad - KW) / stride + 1;
+    a.Cout = Cout;
+    a.out = out;
+    a.out_sw = Cout;
+    a.out_sh = (int64_t)a.Wo * Cout;
+    a.out_sn = (int64_t)a.Ho * a.Wo * Cout;
+    a.res = res;
+    a.res_sw = a.out_sw;
+    a.res_sh = a.out_sh;
+    a.res_sn = a.out_sn;
+    a.KH = KH;
+    a.KW = KW;
+    a.stride = stride;
+    a.pad = pad;
+    a.relu = relu;
+    launch_conv_gemm(a, S(stream));
+  });
+}
+
+int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,
+               int relu, void* stream) {
+  return op_guard([&] {
+    ConvArgs a;
+    a.in = A;
+    a.in_sn = K;
+    a.Cin = K;
+    a.wgt = W;
+    a.ldb = K;
+    a.bias = bias;
+    a.res = res;
+    a.res_sn = N;
+    a.out = C;
+    a.out_sn = N;
+    a.Nimg = M;
+    a.Cout = N;
+    a.relu = relu;
+    launch_conv_gemm(a, S(stream));
+  });
+}
+
+int dd_op_gemm_batched(const float* A, const float* Bm, float* C, int batch, int M, int N, int K, int kn,
+                       void* stream) {
+  return op_guard([&] {
+    ConvArgs a;
+    a.in = A;
+    a.in_sn = K;
+    a.Cin = K;
+    a.wgt = Bm;
+    a.ldb = kn ? N : K;
+    a.b_kn = kn;
+    a.out = C;
+    a.out_sn = N;
+    a.Nimg = M;
+    a.Cout = N;
+    a.batch = batch;
+    a.zdiv = 1;
+    a.in_z1 = (int64_t)M * K;
+    a.w_z1 = (int64_t)K * N;
+    a.out_z1 = (int64_t)M * N;
+    launch_conv_gemm(a, S(stream));
+  });
+}
+
+int dd_op_layernorm(const float* x, const float* res, int res_div, const float* g, const float* b,
+                    const float* film_scale, const float* film_shift, float* y, int rows, int C, void* stream) {
+  return op_guard([&] {
+    launch_layernorm(x, C, res, C, res_div, g, b, film_scale, film_shift, y, C, rows, C, S(stream));
+  });
+}
+
+int dd_op_softmax_rows(float* x, int rows, int L, float scale, void* stream) {
+  return op_guard([&] { launch_softmax_rows(x, L, rows, L, scale, S(stream)); });
+}
+
+int dd_op_bilinear(const float* in, int B, int Hi, int Wi, int C, float* out, int Ho, int Wo, void* stream) {
+  return op_guard([&] {
+    View4 a{const_cast<float*>(in), (int64_t)Hi * Wi * C, (int64_t)Wi * C, C, 1};
+    View4 o{out, (int64_t)Ho * Wo * C, (int64_t)Wo * C, C, 1};
+    launch_bilinear(a, B, Hi, Wi, C, o, Ho, Wo, (float)Hi / (float)Ho, (float)Wi / (float)Wo, 0, S(stream));
+  });
+}
+
+int dd_op_maxpool3x3s2(const float* in, int B, int H, int W, int C, float* out, void* stream) {
+  return op_guard([&] {
+    const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+    launch_maxpool3x3s2(in, out, B, H, W, C, Ho, Wo, S(stream));
+  });
+}
+
+int dd_op_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow, float* out, void* stream) {
+  return op_guard([&] {
+    View4 o{out, (int64_t)oh * ow * C, (int64_t)ow * C, C, 1};
+    launch_avgpool(in, B, H, W, C, oh, ow, o, nullptr, S(stream));
+  });
+}
+
+int dd_op_bev_sample_attn(const float* logits, const float* pts, const float* value, float* out, int B, int Q, int P,
+                          int Hv, int Wv, int C, void* stream) {
+  return op_guard([&] {
+    launch_bev_sample_attn(logits, pts, value, out, B, Q, P, Hv, Wv, C, 1.0f / 32.0f, 1.0f / 32.0f, S(stream));
+  });
+}
+
+int dd_op_mha_small(const float* q, const float* k, const float* v, float* out, int B, int Lq, int Lk, int nh, int hd,
+                    void* stream) {
+  return op_guard([&] {
+    const int d = nh * hd;
+    launch_mha_small(q, d, k, v, d, out, d, B, Lq, Lk, nh, hd, (int64_t)Lq * d, (int64_t)Lk * d, (int64_t)Lq * d,
+                     S(stream));
+  });
+}
+
+}  // extern "C"

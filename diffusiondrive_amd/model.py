@@ -1,0 +1,186 @@
+"""Host-side model object over the ddmi C ABI: the MI355X replacement of ``V2TransfuserModel``.
+
+``DiffusionDriveModel.forward(features)`` has the reference's contract
+(transfuser_model_v2.py:98-162, eval mode): a feature dict with ``camera_feature``
+(B,3,256,1024), ``lidar_feature`` (B,1,256,256), ``status_feature`` (B,8) in, a dict with
+``trajectory`` (B,8,3) out (plus ``bev_semantic_map`` / ``agent_states`` / ``agent_labels`` when
+``heads=True``). The forward runs entirely in ``libddmi.so`` on the GPU; PyTorch only provides
+device memory and the stream. There is no CPU fallback: without the library or a GPU it raises.
+"""
+import ctypes
+from typing import Dict, Mapping, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import TransfuserConfig
+from .schema import state_dict_schema
+from .weights import pack_blob, strip_prefix
+
+ARCH_CODE = {"resnet34": 34, "resnet50": 50}
+
+
+def make_dd_config(cfg: TransfuserConfig) -> _lib.DDConfig:
+    c = _lib.DDConfig()
+    lib = _lib.load()
+    lib.dd_default_config(c)
+    c.image_arch = ARCH_CODE[cfg.image_architecture]
+    c.lidar_arch = ARCH_CODE[cfg.lidar_architecture]
+    c.cam_h, c.cam_w = cfg.camera_height, cfg.camera_width
+    c.lidar_h, c.lidar_w = cfg.lidar_resolution_height, cfg.lidar_resolution_width
+    c.lidar_channels = cfg.lidar_in_channels
+    c.num_modes = cfg.num_modes
+    c.num_poses = cfg.trajectory_sampling.num_poses
+    c.trunc_timestep = cfg.trunc_timestep
+    c.step_span = cfg.step_span
+    return c
+
+
+def check_state_dict(sd: Mapping[str, object], cfg: TransfuserConfig, strict: bool = True):
+    """Key / shape check against the reference schema (load_state_dict(strict=True) semantics,
+    transfuser_agent.py:94-106). Returns (missing, unexpected); raises on mismatch if strict."""
+    schema = {k: tuple(s) for k, s, _ in state_dict_schema(cfg)}
+    missing = [k for k in schema if k not in sd]
+    unexpected = [k for k in sd if k not in schema]
+    bad = [k for k in schema if k in sd and tuple(np.shape(np.asarray(_to_np(sd[k])))) != schema[k]]
+    if strict and (missing or unexpected or bad):
+        raise RuntimeError(
+            f"Error(s) in loading state_dict: missing={missing[:5]}{'...' if len(missing) > 5 else ''} "
+            f"unexpected={unexpected[:5]} shape_mismatch={bad[:5]}")
+    return missing, unexpected
+
+
+def _to_np(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu().numpy()
+    return np.asarray(v)
+
+
+class DiffusionDriveModel:
+    """The DiffusionDrive inference forward on one MI355X (one handle per process/device)."""
+
+    def __init__(self, config: Optional[TransfuserConfig] = None, state_dict: Optional[Mapping] = None,
+                 device: Optional[int] = None):
+        self.config = config or TransfuserConfig()
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.DDMIUnavailable("DiffusionDriveModel needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self._h = None
+        if state_dict is not None:
+            self.load_state_dict(state_dict)
+
+    # ------------------------------------------------------------------ weights
+    def load_state_dict(self, state_dict: Mapping, strict: bool = True):
+        sd = strip_prefix(state_dict)
+        check_state_dict(sd, self.config, strict)
+        blob = pack_blob({k: _to_np(v) for k, v in sd.items()})
+        cfg = make_dd_config(self.config)
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.dd_create(ctypes.byref(cfg), ctypes.cast(buf, ctypes.c_void_p), len(blob),
+                                          self.device, ctypes.byref(h)), self.lib)
+        del buf
+        self.close()
+        self._h = h
+        return self
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            self.lib.dd_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("DiffusionDriveModel has no weights loaded (call load_state_dict)")
+        return self._h
+
+    # ------------------------------------------------------------------ forward
+    def _dev(self, t, dtype=torch.float32):
+        t = torch.as_tensor(t)
+        return t.to(device=f"cuda:{self.device}", dtype=dtype).contiguous()
+
+    def forward(self, features: Dict[str, torch.Tensor], noise: Optional[torch.Tensor] = None,
+                steps: Optional[int] = None, heads: bool = False, modes: bool = False,
+                stream: Optional[torch.cuda.Stream] = None) -> Dict[str, torch.Tensor]:
+        cfg = self.config
+        cam = features["camera_feature"]
+        out_device = cam.device if isinstance(cam, torch.Tensor) else torch.device("cpu")
+        cam = self._dev(cam)
+        lid = self._dev(features["lidar_feature"])
+        st = self._dev(features["status_feature"])
+        B = st.shape[0]
+        Q, P = cfg.num_modes, cfg.trajectory_sampling.num_poses
+        if tuple(cam.shape) != (B, 3, cfg.camera_height, cfg.camera_width):
+            raise ValueError(f"camera_feature must be (B,3,{cfg.camera_height},{cfg.camera_width}), got {tuple(cam.shape)}")
+        if tuple(lid.shape) != (B, cfg.lidar_in_channels, cfg.lidar_resolution_height, cfg.lidar_resolution_width):
+            raise ValueError(f"lidar_feature has shape {tuple(lid.shape)}")
+        if tuple(st.shape) != (B, 8):
+            raise ValueError(f"status_feature must be (B,8), got {tuple(st.shape)}")
+        if noise is None:
+            # the reference draws its DDIM start noise here (transfuser_model_v2.py:593), on CPU
+            noise = torch.randn((B, Q, P, 2))
+        nz = self._dev(noise)
+        if tuple(nz.shape) != (B, Q, P, 2):
+            raise ValueError(f"noise must be (B,{Q},{P},2), got {tuple(nz.shape)}")
+        dev = cam.device
+        traj = torch.empty((B, P, 3), device=dev)
+        outs = _lib.DDOutputs()
+        outs.trajectory = traj.data_ptr()
+        res = {"trajectory": traj}
+        if modes:
+            res["poses_reg"] = torch.empty((B, Q, P, 3), device=dev)
+            res["poses_cls"] = torch.empty((B, Q), device=dev)
+            outs.poses_reg = res["poses_reg"].data_ptr()
+            outs.poses_cls = res["poses_cls"].data_ptr()
+        if heads:
+            res["bev_semantic_map"] = torch.empty(
+                (B, 7, cfg.lidar_resolution_height // 2, cfg.lidar_resolution_width), device=dev)
+            res["agent_states"] = torch.empty((B, cfg.num_bounding_boxes, 5), device=dev)
+            res["agent_labels"] = torch.empty((B, cfg.num_bounding_boxes), device=dev)
+            outs.bev_semantic_map = res["bev_semantic_map"].data_ptr()
+            outs.agent_states = res["agent_states"].data_ptr()
+            outs.agent_labels = res["agent_labels"].data_ptr()
+        s = stream or torch.cuda.current_stream(dev)
+        _lib.check(self.lib.dd_forward_ex(self.handle, cam.data_ptr(), lid.data_ptr(), st.data_ptr(), nz.data_ptr(),
+                                          B, int(steps or cfg.denoise_steps), ctypes.byref(outs),
+                                          s.cuda_stream), self.lib)
+        if out_device.type != "cuda":
+            res = {k: v.to(out_device) for k, v in res.items()}
+        return res
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------ instrumentation
+    def tap(self, name: str, shape=None) -> torch.Tensor:
+        """Copy a named internal buffer of the last forward (NHWC device layout) to a tensor."""
+        n = ctypes.c_size_t()
+        _lib.check(self.lib.dd_tap(self.handle, name.encode(), None, 0, ctypes.byref(n), None), self.lib)
+        t = torch.empty(n.value, device=f"cuda:{self.device}")
+        _lib.check(self.lib.dd_tap(self.handle, name.encode(), t.data_ptr(), n.value, ctypes.byref(n),
+                                   torch.cuda.current_stream(self.device).cuda_stream), self.lib)
+        return t if shape is None else t[: int(np.prod(shape))].view(*shape)
+
+    def set_profiling(self, on: bool):
+        _lib.check(self.lib.dd_set_profiling(self.handle, int(on)), self.lib)
+
+    def set_graph(self, on: bool):
+        _lib.check(self.lib.dd_set_graph(self.handle, int(on)), self.lib)
+
+    def reset_stats(self):
+        _lib.check(self.lib.dd_reset_stats(self.handle), self.lib)
+
+    def kernel_stats(self, kernel: str):
+        ms, n, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+        _lib.check(self.lib.dd_kernel_stats(self.handle, kernel.encode(), ctypes.byref(ms), ctypes.byref(n),
+                                            ctypes.byref(fl)), self.lib)
+        return {"ms": ms.value, "launches": n.value, "flops": fl.value}

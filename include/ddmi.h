@@ -1,0 +1,126 @@
+/* ddmi — MI355X-native DiffusionDrive planner hot path: C ABI.
+ *
+ * The boundary the reference's agent API would bind for its inference forward. Every entry
+ * point takes plain pointers and sizes (device pointers for tensors, hipStream_t passed as
+ * void*), returns 0 on success or a negative code, and records a message for dd_last_error().
+ * No torch types cross this boundary. Reference interfaces each entry replaces:
+ *
+ *   dd_create   <- TransfuserAgent.__init__ + initialize()        transfuser_agent.py:38-57,94-106
+ *                  (V2TransfuserModel construction, strict state_dict load with the
+ *                  `agent.` / `_transfuser_model.` prefixes already stripped by the caller)
+ *   dd_forward  <- TransfuserAgent.forward -> V2TransfuserModel.forward (eval)
+ *                                                                  transfuser_agent.py:120-125,
+ *                                                                  transfuser_model_v2.py:98-162,578-641
+ *   dd_forward_ex  same, with the full output dict (bev_semantic_map, agent_states, agent_labels,
+ *                  all-mode poses) of transfuser_model_v2.py:144-162,165-205
+ *   dd_destroy  <- agent teardown (no reference counterpart; frees device memory)
+ *
+ * Threading: a handle is bound to one device and is not re-entrant; concurrent calls on one
+ * handle must be serialised by the caller (the reference runs one agent per worker process,
+ * run_pdm_score.py:56-57). Different handles are independent.
+ */
+#ifndef DDMI_H_
+#define DDMI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DD_ABI_VERSION 1
+
+#define DD_OK 0
+#define DD_ERR_INVALID -1   /* bad argument / shape / missing or mis-shaped weight */
+#define DD_ERR_RUNTIME -2   /* HIP runtime failure */
+
+typedef struct dd_handle dd_handle;
+
+/* Mirrors the TransfuserConfig fields the hot path reads (transfuser_config.py:10-149). */
+typedef struct dd_config {
+  int abi_version;     /* DD_ABI_VERSION */
+  int image_arch;      /* 34 = resnet34 (default), 50 = resnet50 (nuScenes-style config C4) */
+  int lidar_arch;      /* 34 */
+  int cam_h, cam_w;    /* 256, 1024 */
+  int lidar_h, lidar_w;/* 256, 256 */
+  int lidar_channels;  /* 1 (use_ground_plane = False) */
+  int num_modes;       /* 20 anchors */
+  int num_poses;       /* 8 */
+  int trunc_timestep;  /* 8  (transfuser_model_v2.py:594) */
+  int step_span;       /* 20 (transfuser_model_v2.py:585) */
+} dd_config;
+
+/* Optional outputs of dd_forward_ex (device pointers; NULL = not requested). */
+typedef struct dd_outputs {
+  float* trajectory;       /* B x P x 3  [x, y, heading]  (required) */
+  float* poses_reg;        /* B x Q x P x 3, last step / last layer */
+  float* poses_cls;        /* B x Q */
+  float* bev_semantic_map; /* B x 7 x (lidar_h/2) x lidar_w, NCHW */
+  float* agent_states;     /* B x 30 x 5 */
+  float* agent_labels;     /* B x 30 */
+} dd_outputs;
+
+/* Fill *cfg with the reference defaults. */
+void dd_default_config(dd_config* cfg);
+
+/* Parse a DDW1 weight blob (diffusiondrive_amd/weights.py:pack_blob; reference state_dict key
+ * schema without the `_transfuser_model.` prefix), fold BatchNorm, re-layout for the kernels and
+ * upload to `device`. Missing or mis-shaped keys are an error (strict load). */
+int dd_create(const dd_config* cfg, const void* weights_blob, size_t blob_bytes, int device, dd_handle** out);
+
+/* One eval forward of B scenes. Inputs are device pointers in the reference layouts:
+ * camera (B,3,cam_h,cam_w), lidar (B,C,lidar_h,lidar_w), status (B,8), noise (B,Q,P,2)
+ * (the DDIM start noise the reference draws with torch.randn, transfuser_model_v2.py:593).
+ * steps = number of truncated DDIM steps (2 in the reference). out_modes / out_cls may be NULL. */
+int dd_forward(dd_handle* h, const float* camera, const float* lidar, const float* status, const float* noise,
+               int B, int steps, float* out_traj, float* out_modes, float* out_cls, void* stream);
+
+int dd_forward_ex(dd_handle* h, const float* camera, const float* lidar, const float* status, const float* noise,
+                  int B, int steps, const dd_outputs* outs, void* stream);
+
+int dd_destroy(dd_handle* h);
+
+/* Last error message of the calling thread ("" if none). */
+const char* dd_last_error(void);
+
+/* ---- instrumentation (bench / tests) ---------------------------------------------------- */
+/* Enable per-kernel HIP-event timing (disables graph replay while on). */
+int dd_set_profiling(dd_handle* h, int enable);
+int dd_reset_stats(dd_handle* h);
+/* Accumulated stats of one kernel class ("conv_gemm", "layernorm", ...): total device ms,
+ * launches and algorithmic FLOPs (conv_gemm) since the last reset. Synchronises pending events. */
+int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long long* launches, double* flops);
+/* Enable / disable hipGraph capture + replay of the forward (default on). */
+int dd_set_graph(dd_handle* h, int enable);
+/* Copy a named internal buffer (e.g. "p3", "keyval", "cross_bev", "reg_s0l1") of the last
+ * forward into dst (device pointer), at most `count` floats; *actual = buffer length. */
+int dd_tap(dd_handle* h, const char* name, float* dst, size_t count, size_t* actual, void* stream);
+
+/* ---- single-op entry points (parity tests of individual kernels) ---------------------------- */
+/* Last error message of a dd_op_* call on the calling thread. */
+const char* dd_op_last_error(void);
+/* NHWC conv: in (B,H,W,Cin), wgt (Cout,KH,KW,Cin), optional bias (Cout), res (B,Ho,Wo,Cout). */
+int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
+                 const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream);
+/* C (M,N) = A (M,K) . W(N,K)^T [+ bias] [+ res (M,N)] [relu] */
+int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,
+               int relu, void* stream);
+/* Batched C_z (M,N) = A_z (M,K) . B_z, B_z (K,N) row-major (kn = 1) or (N,K) (kn = 0). */
+int dd_op_gemm_batched(const float* A, const float* Bm, float* C, int batch, int M, int N, int K, int kn,
+                       void* stream);
+int dd_op_layernorm(const float* x, const float* res, int res_div, const float* g, const float* b,
+                    const float* film_scale, const float* film_shift, float* y, int rows, int C, void* stream);
+int dd_op_softmax_rows(float* x, int rows, int L, float scale, void* stream);
+int dd_op_bilinear(const float* in, int B, int Hi, int Wi, int C, float* out, int Ho, int Wo, void* stream);
+int dd_op_maxpool3x3s2(const float* in, int B, int H, int W, int C, float* out, void* stream);
+int dd_op_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow, float* out, void* stream);
+int dd_op_bev_sample_attn(const float* logits, const float* pts, const float* value, float* out, int B, int Q,
+                          int P, int Hv, int Wv, int C, void* stream);
+int dd_op_mha_small(const float* q, const float* k, const float* v, float* out, int B, int Lq, int Lk, int nh,
+                    int hd, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DDMI_H_ */

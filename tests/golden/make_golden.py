@@ -1,0 +1,152 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REFERENCE DiffusionDrive model (build container only).
+
+Imports ``navsim.agents.diffusiondrive.transfuser_model_v2`` from ``/root/reference`` with the
+offline shims in ``refshim``, loads the seeded synthetic state dict
+(``diffusiondrive_amd.weights.seeded_state_dict``) strictly, and records, for each case:
+
+* the full eval-mode outputs: ``trajectory`` (B,8,3), ``agent_states``, ``agent_labels``,
+  a strided sample + checksum of ``bev_semantic_map``;
+* every decoder call's ``poses_reg`` / ``poses_cls`` (2 steps × 2 layers);
+* checksums + strided samples of intermediates (trunk stages, p3, bev feature, keyval,
+  cross-BEV map, tf-decoder output, value_proj maps, grid-sample aggregates).
+
+Noise is the reference's own draw: ``torch.manual_seed(seed)`` right before ``forward``
+(transfuser_model_v2.py:593 is the only RNG consumer). Inputs are regenerated from the seed
+by ``synthetic_inputs`` and their checksums are stored so tests can confirm regeneration.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Writes tests/golden/ref_b{B}_s{seed}.npz and tests/golden/state_dict_schema.json.
+Nothing of the reference's source is copied; only data (inputs/outputs) is stored.
+"""
+import json
+import os
+import sys
+import tempfile
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from diffusiondrive_amd.config import TransfuserConfig  # noqa: E402
+from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs  # noqa: E402
+
+CASES = [(1, 11), (4, 1234)]
+WEIGHT_SEED = 0
+MAX_SAMPLES = 4096
+
+
+def summarize(t: torch.Tensor):
+    a = t.detach().double().reshape(-1).numpy()
+    stride = max(1, a.size // MAX_SAMPLES)
+    return {"sum": np.array(a.sum()), "abssum": np.array(np.abs(a).sum()),
+            "stride": np.array(stride), "sample": a[::stride].astype(np.float32),
+            "shape": np.array(t.shape, dtype=np.int64)}
+
+
+def main():
+    import refshim
+    refshim.install_stub_finder()
+    sys.path.insert(0, REF)
+    from navsim.agents.diffusiondrive.transfuser_config import TransfuserConfig as RefConfig
+    from navsim.agents.diffusiondrive.transfuser_model_v2 import V2TransfuserModel
+
+    cfg = TransfuserConfig()
+    sd_np = seeded_state_dict(cfg, WEIGHT_SEED)
+    with tempfile.TemporaryDirectory() as td:
+        anchor_path = os.path.join(td, "anchors.npy")
+        np.save(anchor_path, sd_np["_trajectory_head.plan_anchor"])
+        rcfg = RefConfig()
+        rcfg.plan_anchor_path = anchor_path
+        model = V2TransfuserModel(rcfg)
+    ref_sd = model.state_dict()
+    schema = [[k, list(v.shape)] for k, v in ref_sd.items()]
+    with open(os.path.join(HERE, "state_dict_schema.json"), "w") as f:
+        json.dump(schema, f, indent=0)
+    model.load_state_dict({k: torch.as_tensor(v) for k, v in sd_np.items()}, strict=True)
+    model.eval()
+    torch.set_num_threads(8)
+
+    for B, seed in CASES:
+        inp = synthetic_inputs(B, seed, cfg)
+        cap = {}
+        calls = {"layer": 0, "vp": 0, "gs": 0}
+        hooks = []
+
+        def save(name, t):
+            cap[name] = t.detach().clone()
+
+        bb = model._backbone
+        for i in range(4):
+            hooks.append(getattr(bb.image_encoder, f"layer{i + 1}").register_forward_hook(
+                lambda m, a, o, i=i: save(f"img_l{i + 1}", o)))
+            hooks.append(getattr(bb.lidar_encoder, f"layer{i + 1}").register_forward_hook(
+                lambda m, a, o, i=i: save(f"lid_l{i + 1}", o)))
+        def bbhook(m, a, o):
+            save("p3", o[0])
+            save("bev_feature", o[1])
+        hooks.append(bb.register_forward_hook(bbhook))
+        hooks.append(model._tf_decoder.register_forward_pre_hook(lambda m, a: save("keyval", a[1])))
+        hooks.append(model._tf_decoder.register_forward_hook(lambda m, a, o: save("query_out", o)))
+        hooks.append(model.bev_proj.register_forward_hook(lambda m, a, o: save("cross_bev_tokens", o)))
+        th = model._trajectory_head
+        for l, layer in enumerate(th.diff_decoder.layers):
+            def lhook(m, a, o):
+                n = calls["layer"]
+                s, ll = divmod(n, len(th.diff_decoder.layers))
+                save(f"reg_s{s}l{ll}", o[0])
+                save(f"cls_s{s}l{ll}", o[1])
+                calls["layer"] += 1
+            hooks.append(layer.register_forward_hook(lhook))
+
+            def vhook(m, a, o, l=l):
+                n = calls["vp"]
+                save(f"value_call{n}_l{l}", o)
+                calls["vp"] += 1
+            hooks.append(layer.cross_bev_attention.value_proj.register_forward_hook(vhook))
+
+            def ghook(m, a):
+                n = calls["gs"]
+                s, ll = divmod(n, len(th.diff_decoder.layers))
+                save(f"gs_s{s}l{ll}", a[0])
+                calls["gs"] += 1
+            hooks.append(layer.cross_bev_attention.output_proj.register_forward_pre_hook(ghook))
+
+        feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+        torch.manual_seed(seed)
+        with torch.no_grad():
+            out = model(feats)
+        for h in hooks:
+            h.remove()
+
+        rec = {"batch": np.array(B), "seed": np.array(seed), "weight_seed": np.array(WEIGHT_SEED)}
+        for k in ("camera_feature", "lidar_feature", "status_feature", "noise"):
+            a = inp[k].astype(np.float64)
+            rec[f"in_{k}_sum"] = np.array(a.sum())
+            rec[f"in_{k}_abssum"] = np.array(np.abs(a).sum())
+        rec["status_feature"] = inp["status_feature"]
+        rec["noise"] = inp["noise"]
+        rec["trajectory"] = out["trajectory"].numpy()
+        rec["agent_states"] = out["agent_states"].numpy()
+        rec["agent_labels"] = out["agent_labels"].numpy()
+        for k, v in summarize(out["bev_semantic_map"]).items():
+            rec[f"tap_bev_semantic_map_{k}"] = v
+        for name, t in cap.items():
+            if name.startswith(("reg_", "cls_")):
+                rec[name] = t.numpy()
+            else:
+                for k, v in summarize(t).items():
+                    rec[f"tap_{name}_{k}"] = v
+        path = os.path.join(HERE, f"ref_b{B}_s{seed}.npz")
+        np.savez_compressed(path, **rec)
+        print(f"wrote {path}: traj[0,0]={rec['trajectory'][0, 0]}, taps={sorted(cap)}")
+
+
+if __name__ == "__main__":
+    main()

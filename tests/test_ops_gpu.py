@@ -1,0 +1,185 @@
+"""Per-kernel parity on the GPU: each ddmi kernel (called through the C ABI) vs a plain
+PyTorch-CPU fp32 reference of the same op on the same seeded inputs.
+
+Tolerances: fp32 MFMA is an exact fp32 fma chain that differs from the CPU only in summation
+order -> relative error ~1e-6 of sum|a*b|; we assert max|err| <= 2e-5 * (1 + max|ref|) for
+contractions and 1e-5 for elementwise / reduction kernels.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from diffusiondrive_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def g(t):
+    """Device copy. Callers must keep the returned tensor alive until the op has run: a temporary
+    passed as ``g(x).data_ptr()`` is freed (and its memory reused) before the kernel executes."""
+    return t.to(DEV).contiguous()
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    gen = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=gen) * scale
+
+
+def ok(rc, lib):
+    _lib.check(rc, lib, op=True)
+    torch.cuda.synchronize()
+
+
+def close(a, ref, tol):
+    a = a.detach().cpu().double()
+    ref = ref.detach().cpu().double()
+    err = (a - ref).abs().max().item()
+    lim = tol * (1.0 + ref.abs().max().item())
+    assert err <= lim, f"max err {err:.3e} > {lim:.3e}"
+    return err
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p,relu,res", [
+    (2, 16, 24, 64, 64, 3, 1, 1, True, True),     # BasicBlock conv2 (+residual)
+    (2, 16, 24, 64, 128, 3, 2, 1, True, False),   # stage-entry conv1 (stride 2)
+    (2, 16, 24, 64, 128, 1, 2, 0, False, False),  # downsample 1x1/s2
+    (1, 40, 70, 4, 64, 7, 2, 3, True, False),     # stem (3 -> padded 4 channels)
+    (2, 8, 8, 512, 7, 1, 1, 0, False, False),     # tiny Cout (semantic logits)
+    (1, 64, 64, 256, 256, 3, 1, 1, True, False),  # value_proj
+    (3, 5, 7, 320, 40, 1, 1, 0, True, True),      # ragged M / N
+])
+def test_conv2d(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
+    x = rnd(B, Cin, H, W, seed=1)
+    w = rnd(Cout, Cin, k, k, seed=2, scale=1.0 / np.sqrt(Cin * k * k))
+    b = rnd(Cout, seed=3)
+    ref = F.conv2d(x, w, b, s, p)
+    r = rnd(*ref.shape, seed=4) if res else None
+    if res:
+        ref = ref + r
+    if relu:
+        ref = F.relu(ref)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    xin, win, bin_ = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b)
+    rin = g(r.permute(0, 2, 3, 1)) if res else None
+    ok(gpu.dd_op_conv2d(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(),
+                        rin.data_ptr() if res else None, out.data_ptr(), Cout, k, k, s, p, int(relu), None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 2e-5)
+
+
+@pytest.mark.parametrize("M,K,N,relu", [(1, 256, 1024, False), (1280, 256, 256, True), (4096, 320, 256, True),
+                                        (600, 1024, 24, False), (77, 8, 256, False), (1280, 256, 1, False)])
+def test_gemm(gpu, M, K, N, relu):
+    a = rnd(M, K, seed=5)
+    w = rnd(N, K, seed=6, scale=1.0 / np.sqrt(K))
+    b = rnd(N, seed=7)
+    r = rnd(M, N, seed=8)
+    ref = a @ w.T + b + r
+    if relu:
+        ref = F.relu(ref)
+    out = torch.empty(M, N, device=DEV)
+    ad, wd, bd, rd = g(a), g(w), g(b), g(r)
+    ok(gpu.dd_op_gemm(ad.data_ptr(), M, K, wd.data_ptr(), bd.data_ptr(), rd.data_ptr(), out.data_ptr(), N,
+                      int(relu), None), gpu)
+    close(out, ref, 2e-5)
+
+
+@pytest.mark.parametrize("batch,M,N,K,kn", [(8, 320, 320, 16, 0), (8, 320, 16, 320, 1), (4, 320, 128, 320, 1),
+                                             (3, 70, 50, 36, 0)])
+def test_gemm_batched(gpu, batch, M, N, K, kn):
+    a = rnd(batch, M, K, seed=9)
+    bm = rnd(batch, K, N, seed=10) if kn else rnd(batch, N, K, seed=10)
+    ref = a @ (bm if kn else bm.transpose(1, 2))
+    out = torch.empty(batch, M, N, device=DEV)
+    ad, bd = g(a), g(bm)
+    ok(gpu.dd_op_gemm_batched(ad.data_ptr(), bd.data_ptr(), out.data_ptr(), batch, M, N, K, kn, None), gpu)
+    close(out, ref, 2e-5)
+
+
+@pytest.mark.parametrize("rows,C,res_div,film", [(1000, 256, 0, False), (333, 64, 20, True), (50, 2048, 0, False),
+                                                 (20, 1024, 4, False)])
+def test_layernorm(gpu, rows, C, res_div, film):
+    x = rnd(rows, C, seed=11, scale=3.0) + 0.5
+    gam, bet = rnd(C, seed=12), rnd(C, seed=13)
+    res = rnd((rows + res_div - 1) // res_div if res_div else rows, C, seed=14) if res_div else None
+    fs, fb = (rnd(C, seed=15), rnd(C, seed=16)) if film else (None, None)
+    xin = x + (res.repeat_interleave(res_div, 0)[:rows] if res_div else 0)
+    ref = F.layer_norm(xin, (C,), gam, bet, 1e-5)
+    if film:
+        ref = ref * (1 + fs) + fb
+    out = torch.empty(rows, C, device=DEV)
+    keep = [g(t) if t is not None else None for t in (x, res, gam, bet, fs, fb)]
+    p = [t.data_ptr() if t is not None else None for t in keep]
+    ok(gpu.dd_op_layernorm(p[0], p[1], max(res_div, 1), p[2], p[3], p[4], p[5], out.data_ptr(), rows, C, None), gpu)
+    close(out, ref, 1e-5)
+
+
+def test_softmax(gpu):
+    x = rnd(777, 320, seed=17, scale=4.0)
+    ref = torch.softmax(x * 0.125, -1)
+    xg = g(x)
+    ok(gpu.dd_op_softmax_rows(xg.data_ptr(), 777, 320, 0.125, None), gpu)
+    close(xg, ref, 1e-6)
+
+
+@pytest.mark.parametrize("B,Hi,Wi,C,Ho,Wo", [(2, 8, 32, 64, 64, 256), (2, 8, 8, 256, 64, 64), (1, 16, 16, 64, 64, 64),
+                                             (2, 64, 64, 7, 128, 256), (1, 8, 8, 12, 16, 16)])
+def test_bilinear(gpu, B, Hi, Wi, C, Ho, Wo):
+    x = rnd(B, C, Hi, Wi, seed=18)
+    ref = F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=False)
+    out = torch.empty(B, Ho, Wo, C, device=DEV)
+    xd = g(x.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_bilinear(xd.data_ptr(), B, Hi, Wi, C, out.data_ptr(), Ho, Wo, None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 1e-6)
+
+
+def test_maxpool(gpu):
+    x = rnd(2, 64, 37, 50, seed=19)
+    ref = F.max_pool2d(x, 3, 2, 1)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    xd = g(x.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_maxpool3x3s2(xd.data_ptr(), 2, 37, 50, 64, out.data_ptr(), None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 0.0)
+
+
+@pytest.mark.parametrize("H,W,oh,ow", [(64, 256, 8, 32), (16, 16, 8, 8), (8, 32, 8, 32)])
+def test_avgpool(gpu, H, W, oh, ow):
+    x = rnd(2, 64, H, W, seed=20)
+    ref = F.adaptive_avg_pool2d(x, (oh, ow))
+    out = torch.empty(2, oh, ow, 64, device=DEV)
+    xd = g(x.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_avgpool(xd.data_ptr(), 2, H, W, 64, oh, ow, out.data_ptr(), None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 1e-6)
+
+
+def test_bev_sample_attn(gpu):
+    B, Q, P, H, W, C = 3, 20, 8, 64, 64, 256
+    logits = rnd(B, Q, P, seed=21, scale=2.0)
+    pts = rnd(B, Q, P, 2, seed=22, scale=20.0)
+    pts[0, 0, 0] = torch.tensor([40.0, -50.0])  # outside the BEV: zero padding
+    pts[0, 0, 1] = torch.tensor([31.7, 31.9])   # partially outside
+    value = rnd(B, C, H, W, seed=23)
+    grid = torch.stack([pts[..., 1] / 32.0, pts[..., 0] / 32.0], -1)
+    s = F.grid_sample(value, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
+    ref = (torch.softmax(logits, -1).unsqueeze(1) * s).sum(-1).permute(0, 2, 1)
+    out = torch.empty(B, Q, C, device=DEV)
+    ld, pd, vd = g(logits), g(pts), g(value.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_bev_sample_attn(ld.data_ptr(), pd.data_ptr(), vd.data_ptr(), out.data_ptr(), B, Q, P, H, W, C,
+                                 None), gpu)
+    close(out, ref, 1e-5)
+
+
+@pytest.mark.parametrize("Lq,Lk", [(31, 31), (31, 65), (20, 30), (20, 1), (5, 128)])
+def test_mha_small(gpu, Lq, Lk):
+    B, nh, hd = 3, 8, 32
+    q, k, v = rnd(B, Lq, nh * hd, seed=24), rnd(B, Lk, nh * hd, seed=25), rnd(B, Lk, nh * hd, seed=26)
+    qh = q.view(B, Lq, nh, hd).transpose(1, 2)
+    kh = k.view(B, Lk, nh, hd).transpose(1, 2)
+    vh = v.view(B, Lk, nh, hd).transpose(1, 2)
+    ref = (torch.softmax(qh @ kh.transpose(-1, -2) / np.sqrt(hd), -1) @ vh).transpose(1, 2).reshape(B, Lq, nh * hd)
+    out = torch.empty(B, Lq, nh * hd, device=DEV)
+    qd, kd, vd = g(q), g(k), g(v)
+    ok(gpu.dd_op_mha_small(qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), B, Lq, Lk, nh, hd, None), gpu)
+    close(out, ref, 1e-5)
