@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: DiffusionDrive eval forward (ResNet-34 + LiDAR-BEV backbone, 2 truncated DDIM
+steps) on MI355X, scenes/s at batch 64 per GPU (BASELINE.json metric / configs[1], weak scaling
+over 1/2/4/8 GPUs with one RCCL all_gather of the predicted trajectories per step).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+A step = one forward of B synthetic scenes resident in HBM (+ the all_gather when N > 1).
+Rank 0 prints ONE JSON line. Also reported:
+  * roofline: the dominant kernel (conv_gemm: every conv / GEMM of the path on fp32 MFMA),
+    algorithmic FLOP per launch / average launch time from HIP events recorded on the kernel's
+    stream during a profiled replay of the timed workload; peak = 157.3 TFLOP/s (fp32 MFMA dense,
+    MI355X_MICROARCH.md).
+  * cpu_baseline: the golden-pinned CPU oracle (oracle/, PyTorch-CPU fp32) timed on this host
+    on a bounded sample of the same workload (rank 0, N = 1 only); its outputs double as the
+    waypoint-L2 parity check of the GPU result on those scenes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+CANONICAL_GFLOP_PER_SCENE_2STEP = 65.27  # SURVEY.md §8d (value_proj once per layer)
+FP32_MFMA_PEAK_TFLOPS = 157.3            # MI355X dense fp32 MFMA (= vector) peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=64, help="scenes per GPU")
+    p.add_argument("--denoise-steps", type=int, default=2)
+    p.add_argument("--cpu-sample", type=int, default=64, help="scenes in the CPU-oracle baseline sample")
+    p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--arch", default="resnet34")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{local}")
+
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
+
+    cfg = TransfuserConfig(image_architecture=args.arch)
+    sd = seeded_state_dict(cfg, 0)
+    model = DiffusionDriveModel(cfg, sd, device=local)
+    B = args.batch
+    inp = synthetic_inputs(B, 1234 + rank, cfg)
+    feats = {k: torch.from_numpy(inp[k]).to(dev) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    noise = torch.from_numpy(inp["noise"]).to(dev)
+    from diffusiondrive_amd.dist import ScenePlanner
+    planner = ScenePlanner(lambda f, nz: model.forward(f, noise=nz, steps=args.denoise_steps)["trajectory"])
+
+    def step():
+        # per-rank shard of the global batch (weak scaling) + one RCCL all_gather of trajectories
+        return planner.gather(planner.fn(feats, noise))
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    scenes_per_s = B * world * args.steps / elapsed
+    traj_gpu = out[rank * B:(rank + 1) * B].detach().cpu().numpy()
+
+    # ---- roofline of the dominant kernel: a profiled replay of the same workload (HIP events
+    # around every conv_gemm launch on the handle's stream)
+    model.set_profiling(True)
+    model.reset_stats()
+    prof_steps = max(1, min(args.steps, 5))
+    for _ in range(prof_steps):
+        model.forward(feats, noise=noise, steps=args.denoise_steps)
+    torch.cuda.synchronize()
+    st = model.kernel_stats("conv_gemm")
+    other = {k: model.kernel_stats(k) for k in ("layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
+                                                 "misc")}
+    model.set_profiling(False)
+    avg_ms = st["ms"] / max(st["launches"], 1)
+    flops_per_launch = st["flops"] / max(st["launches"], 1)
+    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    total_prof_ms = st["ms"] + sum(v["ms"] for v in other.values())
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_conv_gemm.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "scenes/s at batch 64, 2 denoise steps, 1/2/4/8 MI355X; waypoint L2 vs ref",
+        "value": round(scenes_per_s, 3),
+        "unit": "scenes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded camera/LiDAR/status/noise; seeded random weights of the reference architecture)",
+        "config": {
+            "workload": f"DiffusionDrive eval forward: {args.arch} camera + ResNet-34 LiDAR-BEV backbone, "
+                        f"GPT fusion x4, tf decoder, truncated diffusion decoder {args.denoise_steps} DDIM steps x 2 "
+                        f"layers, 20 modes; batch {B} scenes per GPU",
+            "batch_per_gpu": B,
+            "global_batch": B * world,
+            "denoise_steps": args.denoise_steps,
+            "parallelism": f"dp{world} (scene sharding, RCCL all_gather of trajectories)",
+            "graph": True,
+        },
+        "roofline": {
+            "kernel": "conv_gemm (implicit-GEMM conv / GEMM, fp32 MFMA 32x32x2)",
+            "bound": "mfma",
+            "achieved": round(achieved, 3),
+            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "launches_per_step": st["launches"] // prof_steps,
+            "avg_launch_ms": round(avg_ms, 5),
+            "gflop_per_launch": round(flops_per_launch / 1e9, 4),
+            "share_of_device_time": round(st["ms"] / total_prof_ms, 4) if total_prof_ms else None,
+        },
+        "whole_forward": {
+            "gflop_per_scene": CANONICAL_GFLOP_PER_SCENE_2STEP if args.denoise_steps == 2 else None,
+            "tflops": round(scenes_per_s / world * CANONICAL_GFLOP_PER_SCENE_2STEP / 1e3, 3)
+            if args.denoise_steps == 2 else None,
+        },
+    }
+    if result["whole_forward"]["tflops"] is not None:
+        result["whole_forward"]["frac_of_fp32_peak"] = round(result["whole_forward"]["tflops"] / FP32_MFMA_PEAK_TFLOPS,
+                                                             4)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, cfg, sd, inp, traj_gpu)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, cfg, sd, inp, traj_gpu):
+    """Golden-pinned CPU oracle on a bounded sample (first `cpu_sample` scenes of the batch)."""
+    from oracle.model import OracleModel
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    S = min(args.cpu_sample, inp["status_feature"].shape[0])
+    om = OracleModel(sd, cfg)
+    sl = {k: inp[k][:S] for k in ("camera_feature", "lidar_feature", "status_feature", "noise")}
+    om.forward(sl["camera_feature"][:1], sl["lidar_feature"][:1], sl["status_feature"][:1], sl["noise"][:1],
+               steps=args.denoise_steps, heads=False)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_reps):
+        ref = om.forward(sl["camera_feature"], sl["lidar_feature"], sl["status_feature"], sl["noise"],
+                         steps=args.denoise_steps, heads=False)["trajectory"].numpy()
+    dt = time.perf_counter() - t0
+    d = (traj_gpu[:S, :, :2].astype(np.float64) - ref[..., :2].astype(np.float64)).reshape(S, -1)
+    l2 = float(np.sqrt((d ** 2).sum(-1)).max())
+    cpu_name = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(S * args.cpu_reps / dt, 4),
+        "unit": "scenes/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{S} scenes x {args.cpu_reps} reps of the same synthetic batch (oracle/model.py, PyTorch-CPU "
+                  f"fp32, {threads} threads, {cpu_name})",
+        "seconds": round(dt, 2),
+        "waypoint_l2_gpu_vs_oracle": l2,
+    }
+
+
+if __name__ == "__main__":
+    main()
