@@ -10,12 +10,18 @@
 //
 // Tiling (MI355X-first):
 //  * 256-thread workgroups = 4 wave64 as 2x2; each wave owns WTM x WTN 32x32 MFMA tiles.
-//  * K staged in BK = 32 chunks; global -> registers (float4, NHWC channel slices) -> LDS,
-//    double-buffered so the next chunk's HBM/L2 loads overlap the current chunk's MFMAs.
+//  * K staged in BK = 32 chunks; HBM/L2 -> registers (16-B buffer loads of NHWC channel slices)
+//    -> LDS, double-buffered: chunk k+1's loads are in flight while chunk k's MFMAs run.
+//  * Operand loads are raw buffer loads with 32-bit offsets. Conv zero padding and ragged
+//    M/N/K edges use an out-of-range offset (>= num_records) so the hardware returns zeros:
+//    no branch, no select on data, every load unconditional (a predicated `ok ? load : 0` makes
+//    hipcc branch per load and wait vmcnt(0) after each, serialising the prefetch).
 //  * LDS rows padded to 36 floats (144 B): the 16-lane groups of ds_read_b128 hit 16 distinct
 //    16-B slots (row stride 9 slots, coprime with 16) -> conflict-free fragment reads.
 //  * k-permutation: within each 8-k group, MFMA step s consumes k = {s, 4+s} (lane halves), so one
 //    ds_read_b128 per operand feeds 4 consecutive MFMAs (A[i][4h..4h+3], B[j][4h..4h+3]).
+//  * XCD-aware tile order: blocks b, b+8, b+16, ... share one XCD's L2 under round-robin dispatch,
+//    so they get consecutive tiles (same A rows / neighbouring conv halos) — speed only.
 //  * Epilogue fused: alpha, bias (BN folded at load time), residual, ReLU, strided NHWC store
 //    (channel offsets / strides let convs write straight into concat buffers and token slabs).
 #include "common.h"
@@ -26,19 +32,36 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
 constexpr int LDSK = BK + 4;
+constexpr uint32_t kOOB = 0x80000000u;  // byte offset >= num_records -> buffer load returns 0
+
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const float* base) {
+  // raw buffer, stride 0, num_records = 2 GiB (every in-range offset of a launch is < 2^31 B)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)kOOB, 0x00020000);
+}
+
+__device__ inline float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0);
+  return *reinterpret_cast<float4*>(&v);
+}
 
 template <int WTM, int WTN, int BKN>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a, int M, int K, int n_tiles_n) {
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a, int M, int K, int n_tiles_m,
+                                                           int n_tiles_n) {
   constexpr int BM = 2 * WTM * 32;
   constexpr int BN = 2 * WTN * 32;
   constexpr int A_LD = BM * BK / 4 / 256;
   constexpr int B_LD = BN * BK / 4 / 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDSK];
-  float* As = lds;
-  float* Bs = lds + 2 * BM * LDSK;
 
   const int tid = threadIdx.x;
-  const int tile = blockIdx.x;
+  // XCD-aware bijective remap of the linear block id (MI355X: 8 XCDs, round-robin dispatch).
+  const int nblk = n_tiles_m * n_tiles_n;
+  const int bid = blockIdx.x;
+  int tile = bid;
+  if (nblk >= 16) {
+    const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
   const int mt_idx = tile / n_tiles_n;
   const int nt_idx = tile - mt_idx * n_tiles_n;
   const int m0 = mt_idx * BM;
@@ -46,96 +69,91 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a, int M, in
 
   // batched pointer offsets
   const int z = blockIdx.z;
-  const int z1 = z / a.zdiv, z2 = z - (z / a.zdiv) * a.zdiv;
-  const float* __restrict__ in = a.in + z1 * a.in_z1 + z2 * a.in_z2;
-  const float* __restrict__ wgt = a.wgt + z1 * a.w_z1 + z2 * a.w_z2;
-  float* __restrict__ out = a.out + z1 * a.out_z1 + z2 * a.out_z2;
-  const float* __restrict__ res = a.res ? a.res + z1 * a.res_z1 + z2 * a.res_z2 : nullptr;
+  const int z1 = z / a.zdiv, z2 = z - z1 * a.zdiv;
+  const float* in = a.in + z1 * a.in_z1 + z2 * a.in_z2;
+  const float* wgt = a.wgt + z1 * a.w_z1 + z2 * a.w_z2;
+  float* out = a.out + z1 * a.out_z1 + z2 * a.out_z2;
+  const float* res = a.res ? a.res + z1 * a.res_z1 + z2 * a.res_z2 : nullptr;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(in);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(wgt);
 
-  // ---- per-thread A-row decode (fixed across K chunks)
+  const int in_sh = (int)a.in_sh, in_sw = (int)a.in_sw;
+  const int ldb = (int)a.ldb;
+
+  // ---- per-thread A-row decode (fixed across K chunks); element offsets in int32
   const int k4 = (tid & 7) * 4;
-  const float* abase[A_LD];
-  int aih0[A_LD], aiw0[A_LD];
-  bool avalid[A_LD];
+  int arow[A_LD], aih0[A_LD], aiw0[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
-    const int r = (tid >> 3) + 32 * i;
-    const int m = m0 + r;
-    avalid[i] = m < M;
-    const int mm = avalid[i] ? m : 0;
+    const int m = m0 + (tid >> 3) + 32 * i;
+    const bool v = m < M;
+    const int mm = v ? m : 0;
     const int ow = mm % a.Wo;
     const int t2 = mm / a.Wo;
     const int oh = t2 % a.Ho;
     const int n = t2 / a.Ho;
-    abase[i] = in + (int64_t)n * a.in_sn;
-    aih0[i] = oh * a.stride - a.pad;
+    arow[i] = n * (int)a.in_sn;
+    // invalid rows get an origin far outside the image so every tap fails the bounds test
+    aih0[i] = v ? oh * a.stride - a.pad : -(1 << 28);
     aiw0[i] = ow * a.stride - a.pad;
   }
 
   float4 ra[A_LD], rb[B_LD];
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  auto load_chunk = [&](int k0) {
-    const int kk = k0 + k4;
-    const bool kv = kk < K;
-    const int tap = kk / a.Cin;
-    const int ci = kk - tap * a.Cin;
-    const int kh = tap / a.KW;
-    const int kw = tap - kh * a.KW;
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      const int ih = aih0[i] + kh, iw = aiw0[i] + kw;
-      const bool ok = avalid[i] && kv && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      ra[i] = ok ? *reinterpret_cast<const float4*>(abase[i] + ih * a.in_sh + iw * a.in_sw + ci) : zero4;
-    }
-    if constexpr (!BKN) {
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) {
-        const int n = n0 + (tid >> 3) + 32 * i;
-        const bool ok = kv && n < a.Cout;
-        rb[i] = ok ? *reinterpret_cast<const float4*>(wgt + (int64_t)n * a.ldb + kk) : zero4;
-      }
-    } else {
-      constexpr int NF4 = BN / 4;
-      constexpr int RPP = 256 / NF4;
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) {
-        const int kr = k0 + tid / NF4 + RPP * i;
-        const int n = n0 + (tid % NF4) * 4;
-        const bool ok = kr < K && n < a.Cout;  // Cout % 4 == 0 enforced by the launcher
-        rb[i] = ok ? *reinterpret_cast<const float4*>(wgt + (int64_t)kr * a.ldb + n) : zero4;
-      }
-    }
-  };
+#define DD_LOAD_CHUNK(K0)                                                                            \
+  {                                                                                                  \
+    const int kk = (K0) + k4;                                                                        \
+    const bool kv = kk < K;                                                                          \
+    const int tap = kk / a.Cin;                                                                      \
+    const int ci = kk - tap * a.Cin;                                                                 \
+    const int kh = tap / a.KW;                                                                       \
+    const int kw = tap - kh * a.KW;                                                                  \
+    _Pragma("unroll") for (int i = 0; i < A_LD; ++i) {                                               \
+      const int ih = aih0[i] + kh, iw = aiw0[i] + kw;                                                \
+      const bool ok = kv && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;            \
+      const uint32_t off = ok ? (uint32_t)(arow[i] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB;      \
+      ra[i] = bload4(rin, off);                                                                      \
+    }                                                                                                \
+    if constexpr (!BKN) {                                                                            \
+      _Pragma("unroll") for (int i = 0; i < B_LD; ++i) {                                             \
+        const int n = n0 + (tid >> 3) + 32 * i;                                                      \
+        const bool ok = kv && n < a.Cout;                                                            \
+        rb[i] = bload4(rw, ok ? (uint32_t)(n * ldb + kk) * 4u : kOOB);                               \
+      }                                                                                              \
+    } else {                                                                                         \
+      constexpr int NF4 = BN / 4;                                                                    \
+      constexpr int RPP = 256 / NF4;                                                                 \
+      _Pragma("unroll") for (int i = 0; i < B_LD; ++i) {                                             \
+        const int kr = (K0) + tid / NF4 + RPP * i;                                                   \
+        const int n = n0 + (tid % NF4) * 4;                                                          \
+        const bool ok = kr < K && n < a.Cout;                                                        \
+        rb[i] = bload4(rw, ok ? (uint32_t)(kr * ldb + n) * 4u : kOOB);                               \
+      }                                                                                              \
+    }                                                                                                \
+  }
 
-  auto store_chunk = [&](int buf) {
-    float* as = As + buf * BM * LDSK;
-    float* bs = Bs + buf * BN * LDSK;
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<float4*>(as + r * LDSK + k4) = ra[i];
-    }
-    if constexpr (!BKN) {
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) {
-        const int r = (tid >> 3) + 32 * i;
-        *reinterpret_cast<float4*>(bs + r * LDSK + k4) = rb[i];
-      }
-    } else {
-      constexpr int NF4 = BN / 4;
-      constexpr int RPP = 256 / NF4;
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i) {
-        const int kr = tid / NF4 + RPP * i;
-        const int n = (tid % NF4) * 4;
-        bs[(n + 0) * LDSK + kr] = rb[i].x;
-        bs[(n + 1) * LDSK + kr] = rb[i].y;
-        bs[(n + 2) * LDSK + kr] = rb[i].z;
-        bs[(n + 3) * LDSK + kr] = rb[i].w;
-      }
-    }
-  };
+#define DD_STORE_CHUNK(BUF)                                                                          \
+  {                                                                                                  \
+    float* as = lds + (BUF) * BM * LDSK;                                                             \
+    float* bs = lds + 2 * BM * LDSK + (BUF) * BN * LDSK;                                             \
+    _Pragma("unroll") for (int i = 0; i < A_LD; ++i)                                                 \
+      *reinterpret_cast<float4*>(as + ((tid >> 3) + 32 * i) * LDSK + k4) = ra[i];                     \
+    if constexpr (!BKN) {                                                                            \
+      _Pragma("unroll") for (int i = 0; i < B_LD; ++i)                                               \
+        *reinterpret_cast<float4*>(bs + ((tid >> 3) + 32 * i) * LDSK + k4) = rb[i];                   \
+    } else {                                                                                         \
+      constexpr int NF4 = BN / 4;                                                                    \
+      constexpr int RPP = 256 / NF4;                                                                 \
+      _Pragma("unroll") for (int i = 0; i < B_LD; ++i) {                                             \
+        const int kr = tid / NF4 + RPP * i;                                                          \
+        const int n = (tid % NF4) * 4;                                                               \
+        bs[(n + 0) * LDSK + kr] = rb[i].x;                                                           \
+        bs[(n + 1) * LDSK + kr] = rb[i].y;                                                           \
+        bs[(n + 2) * LDSK + kr] = rb[i].z;                                                           \
+        bs[(n + 3) * LDSK + kr] = rb[i].w;                                                           \
+      }                                                                                              \
+    }                                                                                                \
+  }
 
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -150,15 +168,16 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a, int M, in
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nk = (K + BK - 1) / BK;
-  load_chunk(0);
-  store_chunk(0);
+  DD_LOAD_CHUNK(0);
+  DD_STORE_CHUNK(0);
   __syncthreads();
 
   for (int kc = 0; kc < nk; ++kc) {
     const int cur = kc & 1;
-    if (kc + 1 < nk) load_chunk((kc + 1) * BK);
-    const float* as = As + cur * BM * LDSK;
-    const float* bs = Bs + cur * BN * LDSK;
+    const bool more = kc + 1 < nk;
+    if (more) DD_LOAD_CHUNK((kc + 1) * BK);
+    const float* as = lds + cur * BM * LDSK;
+    const float* bs = lds + 2 * BM * LDSK + cur * BN * LDSK;
 #pragma unroll
     for (int g = 0; g < BK / 8; ++g) {
       float4 av[WTM], bv[WTN];
@@ -178,9 +197,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a, int M, in
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
         }
     }
-    if (kc + 1 < nk) store_chunk(cur ^ 1);
+    if (more) DD_STORE_CHUNK(cur ^ 1);
     __syncthreads();
   }
+#undef DD_LOAD_CHUNK
+#undef DD_STORE_CHUNK
 
   // ---- fused epilogue. C/D map of 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
   float bias_v[WTN];
@@ -190,6 +211,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a, int M, in
     ncol[j] = n0 + (wn * WTN + j) * 32 + li;
     bias_v[j] = (a.bias && ncol[j] < a.Cout) ? a.bias[ncol[j]] : 0.f;
   }
+  const int osh = (int)a.out_sh, osw = (int)a.out_sw;
+  const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
 #pragma unroll
   for (int i = 0; i < WTM; ++i) {
 #pragma unroll
@@ -203,15 +226,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a, int M, in
       for (int e = 0; e < 4; ++e) {
         const int m = mbase + e;
         if (m < M) {
-          const int64_t ooff = (int64_t)n * a.out_sn + (int64_t)oh * a.out_sh + (int64_t)ow * a.out_sw;
-          const int64_t roff = (int64_t)n * a.res_sn + (int64_t)oh * a.res_sh + (int64_t)ow * a.res_sw;
+          float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
+          const float* rrow = res ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
 #pragma unroll
           for (int j = 0; j < WTN; ++j) {
             if (ncol[j] < a.Cout) {
               float v = acc[i][j][q * 4 + e] * a.alpha + bias_v[j];
-              if (res) v += res[roff + ncol[j]];
+              if (rrow) v += rrow[ncol[j]];
               if (a.relu) v = fmaxf(v, 0.f);
-              out[ooff + ncol[j]] = v;
+              orow[ncol[j]] = v;
             }
           }
         }
@@ -234,9 +257,9 @@ static void launch_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, a.batch);
   if (a.b_kn)
-    hipLaunchKernelGGL((conv_gemm_kernel<WTM, WTN, 1>), grid, dim3(256), 0, st, a, M, K, ntn);
+    hipLaunchKernelGGL((conv_gemm_kernel<WTM, WTN, 1>), grid, dim3(256), 0, st, a, M, K, ntm, ntn);
   else
-    hipLaunchKernelGGL((conv_gemm_kernel<WTM, WTN, 0>), grid, dim3(256), 0, st, a, M, K, ntn);
+    hipLaunchKernelGGL((conv_gemm_kernel<WTM, WTN, 0>), grid, dim3(256), 0, st, a, M, K, ntm, ntn);
   DD_HIP_CHECK(hipGetLastError());
 }
 
@@ -254,6 +277,14 @@ void launch_conv_gemm(const ConvArgs& a, hipStream_t st) {
   const int M = (int)M64;
   const int K = a.KH * a.KW * a.Cin;
   if (M == 0 || a.Cout == 0) return;
+  // 32-bit buffer offsets: the furthest element a launch touches must stay below 2^31 bytes.
+  const int64_t in_extent = (int64_t)(a.Nimg - 1) * a.in_sn + (int64_t)(a.H - 1) * a.in_sh +
+                            (int64_t)(a.W - 1) * a.in_sw + a.Cin;
+  const int64_t w_extent = a.b_kn ? (int64_t)K * a.ldb : (int64_t)a.Cout * a.ldb;
+  if (in_extent * 4 >= (int64_t)kOOB || w_extent * 4 >= (int64_t)kOOB)
+    throw std::runtime_error("conv_gemm: operand extent >= 2 GiB (split the batch)");
+  if ((int64_t)a.Ho * a.out_sh >= (int64_t(1) << 31) || (int64_t)a.Ho * a.res_sh >= (int64_t(1) << 31))
+    throw std::runtime_error("conv_gemm: per-image output extent too large");
   const int64_t tiles_big = ((M + 127) / 128) * (int64_t)((a.Cout + 127) / 128) * a.batch;
   if (a.Cout <= 64) {
     if (((M + 127) / 128) * (int64_t)a.batch >= 512)
