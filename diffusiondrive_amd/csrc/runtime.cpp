@@ -13,6 +13,8 @@
 //  * the final DDIM step's output is never read (the trajectory comes from poses_reg, :637-641),
 //    so it is skipped.
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -68,6 +70,7 @@ struct PendingEv {
   std::string name;
   double flops;
   hipEvent_t a, b;
+  std::string detail;  // launch shape (profiling only; written to $DDMI_LAUNCH_LOG)
 };
 
 static void trunk_channels(int arch, int ch[5], bool& bottleneck) {
@@ -338,7 +341,7 @@ class Model {
   }
 
   template <class F>
-  void launch(const char* name, double flops, F&& f) {
+  void launch(const char* name, double flops, F&& f, const ConvArgs* shape = nullptr) {
     if (!profiling) {
       f();
       return;
@@ -356,10 +359,20 @@ class Model {
     DD_HIP_CHECK(hipEventRecord(a, st));
     f();
     DD_HIP_CHECK(hipEventRecord(b, st));
-    pending.push_back({name, flops, a, b});
+    std::string detail;
+    if (shape) {
+      const ConvArgs& c = *shape;
+      detail = "M=" + std::to_string((int64_t)c.Nimg * c.Ho * c.Wo) + " N=" + std::to_string(c.Cout) +
+               " K=" + std::to_string(c.KH * c.KW * c.Cin) + " k=" + std::to_string(c.KH) + " s=" +
+               std::to_string(c.stride) + " z=" + std::to_string(c.batch) + " HW=" + std::to_string(c.H) + "x" +
+               std::to_string(c.W);
+    }
+    pending.push_back({name, flops, a, b, detail});
   }
 
   void collect() {
+    const char* log_path = getenv("DDMI_LAUNCH_LOG");
+    FILE* log = log_path ? fopen(log_path, "a") : nullptr;
     for (auto& p : pending) {
       DD_HIP_CHECK(hipEventSynchronize(p.b));
       float ms = 0;
@@ -368,10 +381,12 @@ class Model {
       s.ms += ms;
       s.n += 1;
       s.flops += p.flops;
+      if (log) fprintf(log, "%s\t%s\t%.6g\t%.6f\n", p.name.c_str(), p.detail.c_str(), p.flops, ms);
       ev_pool.push_back(p.a);
       ev_pool.push_back(p.b);
     }
     pending.clear();
+    if (log) fclose(log);
   }
 
   // conv on strided NHWC views
@@ -406,7 +421,7 @@ class Model {
     a.pad = c.pad;
     a.relu = relu;
     const double fl = 2.0 * N * a.Ho * a.Wo * (double)c.cout * c.k * c.k * c.cin_real;
-    launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); });
+    launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
   // contiguous NHWC conv; returns output spatial size
   void conv_c(const Conv& c, const float* in, int N, int H, int Wd, float* out, bool relu, const float* res = nullptr) {
@@ -447,7 +462,7 @@ class Model {
     a.Cout = L.nout;
     a.relu = relu;
     const double fl = 2.0 * G * R * (double)L.nout * L.nin;
-    launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); });
+    launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
 
   void ln(const LNp& p, const float* x, int64_t ldx, float* y, int64_t ldy, int rows, const float* res = nullptr,
@@ -546,7 +561,7 @@ class Model {
         a.w_z2 = hs;
         a.out_z1 = (int64_t)4 * T * T;
         a.out_z2 = (int64_t)T * T;
-        launch("conv_gemm", 2.0 * B * 4 * T * T * hs, [&] { launch_conv_gemm(a, st); });
+        launch("conv_gemm", 2.0 * B * 4 * T * T * hs, [&] { launch_conv_gemm(a, st); }, &a);
       }
       launch("softmax", 0, [&] { launch_softmax_rows(S, T, B * 4 * T, T, 1.0f / std::sqrt((float)hs), st); });
       {  // Y = P V per (scene, head)
@@ -570,7 +585,7 @@ class Model {
         a.w_z2 = hs;
         a.out_z1 = (int64_t)T * C;
         a.out_z2 = hs;
-        launch("conv_gemm", 2.0 * B * 4 * T * T * hs, [&] { launch_conv_gemm(a, st); });
+        launch("conv_gemm", 2.0 * B * 4 * T * T * hs, [&] { launch_conv_gemm(a, st); }, &a);
       }
       gemm(w.proj, Y, C, M, X, C, false, X, C);  // x = x + proj(y)
       ln(w.ln2, X, C, Hb, C, M);
