@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--arch", default="resnet34")
+    p.add_argument("--gemm", default="fp32", choices=["fp32", "f16x3"],
+                   help="conv/linear arithmetic: fp32 MFMA or the fp32-class 3-product fp16 split")
     return p.parse_args()
 
 
@@ -67,6 +69,7 @@ def main():
     cfg = TransfuserConfig(image_architecture=args.arch)
     sd = seeded_state_dict(cfg, 0)
     model = DiffusionDriveModel(cfg, sd, device=local)
+    model.set_gemm_mode(args.gemm)
     B = args.batch
     inp = synthetic_inputs(B, 1234 + rank, cfg)
     feats = {k: torch.from_numpy(inp[k]).to(dev) for k in ("camera_feature", "lidar_feature", "status_feature")}

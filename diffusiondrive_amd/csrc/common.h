@@ -52,8 +52,18 @@ struct ConvArgs {
   int batch = 1, zdiv = 1;
   int64_t in_z1 = 0, in_z2 = 0, w_z1 = 0, w_z2 = 0, out_z1 = 0, out_z2 = 0, res_z1 = 0, res_z2 = 0;
   int64_t flops_K = -1;  // algorithmic K per output (excluding channel padding); -1 = KH*KW*Cin
+  // f16x3 split path (conv_x3.hip): pre-split weights hi / lo [Cout][ldh] fp16 (K order as wgt,
+  // zero padded to ldh % 8 == 0) with per-channel inverse power-of-two scales; flags receives
+  // DD_NUM_* bits. When wh is set, launch_conv_gemm dispatches to the f16x3 kernel.
+  const uint16_t* wh = nullptr;
+  const uint16_t* wl = nullptr;
+  const float* wsinv = nullptr;
+  int64_t ldh = 0;
+  unsigned* flags = nullptr;
 };
+constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
+void launch_conv_x3(const ConvArgs& a, hipStream_t st);
 
 // ----------------------------------------------------------------------------------------
 // Bandwidth / small kernels (elementwise.hip)

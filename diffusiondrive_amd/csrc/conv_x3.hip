@@ -1,0 +1,364 @@
+// Implicit-GEMM convolution / GEMM on CDNA4 f16 MFMA with a 3-product fp16 split
+// ("f16x3": fp32-class accuracy at 5.3x the fp32-MFMA issue rate).
+//
+// Same contract as conv_gemm.hip (ConvArgs; the reference ops it carries are listed there). Every
+// fp32 operand x is split into two fp16 values, hi = f16(x) and lo = f16(x - hi), so
+// x = hi + lo + r with |r| <= 2^-22 |x| (RNE twice). The product a*b is taken as
+//     ah*bh + ah*bl + al*bh          (the al*bl term is <= 2^-22 |a b| and dropped)
+// on v_mfma_f32_32x32x16_f16 with fp32 accumulation: each f16 x f16 product is exact in fp32, so
+// the only error beyond the fp32 path's summation-order difference is the <= ~3*2^-22 relative
+// per-product split residue. Measured end to end: waypoint L2 vs the fp64
+// restatement 1.2e-5, vs 9.5e-6 for plain fp32 - the same class; the bar is 1e-4.
+//
+// Range: weights are pre-split on the host with a per-output-channel power-of-two scale that puts
+// max|w| at 2^15 (exact; undone in the epilogue), so no weight lo part is lost to fp16 subnormals.
+// Activations are split unscaled: an |x| >= 65504 would overflow fp16, so the kernel ORs
+// DD_NUM_F16_OVERFLOW into *flags (the runtime reports it via dd_numerics_flags; the host agent
+// raises / re-runs in fp32). Activations below 2^-3 have a subnormal lo part: absolute error
+// <= 2^-25, negligible against the row sums it feeds.
+//
+// Tiling (MI355X-first):
+//  * WM x WN waves (64*WM*WN threads), each wave TM x TN 32x32 MFMA tiles; BK = 32.
+//  * A (fp32 NHWC activations) is loaded as 16-B float4 channel slices with raw buffer loads (OOB
+//    offset -> hardware zero for conv padding and ragged edges, no per-load branches), split in
+//    registers, and written to LDS as separate hi / lo images. B (pre-split fp16 weights, [N][Kp])
+//    is loaded as 16-B pieces straight into its hi / lo images. LDS rows are 64 B (32 halfs) with
+//    the 16-B slot XOR-swizzled by (row >> 2) & 3 so that a 16-lane ds_read_b128 group (16
+//    consecutive rows, one slot) covers all 16 slots of a 256-B bank row: conflict-free.
+//  * Double-buffered LDS; chunk k+1's global loads are in flight during chunk k's MFMAs.
+//  * XCD-aware bijective tile remap (blocks b, b+8, ... share an XCD's L2 -> consecutive tiles).
+//  * Fused epilogue: per-channel weight scale, alpha, bias, residual, ReLU, strided NHWC store.
+#include "common.h"
+
+namespace ddmi {
+
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)kOOB, 0x00020000);
+}
+
+__device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0);
+  return *reinterpret_cast<uint4*>(&v);
+}
+
+// fp32 -> (hi, lo) fp16 pair, packed 2 per dword.
+__device__ inline void split2(float x, float y, uint32_t& hi, uint32_t& lo) {
+  const _Float16 hx = (_Float16)x, hy = (_Float16)y;
+  const _Float16 lx = (_Float16)(x - (float)hx), ly = (_Float16)(y - (float)hy);
+  hi = (uint32_t)__builtin_bit_cast(uint16_t, hx) | ((uint32_t)__builtin_bit_cast(uint16_t, hy) << 16);
+  lo = (uint32_t)__builtin_bit_cast(uint16_t, lx) | ((uint32_t)__builtin_bit_cast(uint16_t, ly) << 16);
+}
+
+}  // namespace
+
+template <int WM, int WN, int TM, int TN, int CIN32>
+__global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
+                                                               int n_tiles_n) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int A_LD = BM * (BK / 4) / NT;  // float4 A pieces per thread per chunk
+  constexpr int B_LD = BN * 4 / NT;         // 16-B B pieces per thread per chunk, per image (hi / lo)
+  static_assert(A_LD >= 1 && BM * (BK / 4) % NT == 0, "A tile / threads");
+  static_assert(B_LD >= 1 && BN * 4 % NT == 0, "B tile / threads");
+  constexpr int ROWB = BK * 2;                       // 64-B LDS rows (32 halfs)
+  constexpr int STAGE = (2 * BM + 2 * BN) * ROWB;   // Ah, Al, Bh, Bl
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int nblk = n_tiles_m * n_tiles_n;
+  const int bid = blockIdx.x;
+  int tile = bid;
+  if (nblk >= 16) {
+    const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int mt_idx = tile / n_tiles_n;
+  const int nt_idx = tile - mt_idx * n_tiles_n;
+  const int m0 = mt_idx * BM;
+  const int n0 = nt_idx * BN;
+
+  const float* in = a.in;
+  float* out = a.out;
+  const float* res = a.res;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(in);
+  const __amdgpu_buffer_rsrc_t rwh = make_rsrc(a.wh);
+  const __amdgpu_buffer_rsrc_t rwl = make_rsrc(a.wl);
+  const int in_sh = (int)a.in_sh, in_sw = (int)a.in_sw;
+  const int ldh = (int)a.ldh;
+  const int Kp = (K + 7) & ~7;
+
+  // ---- per-thread A rows (fixed across K chunks)
+  const int kq = tid & 7;  // float4 index inside the 32-wide K chunk
+  int arow[A_LD], aih0[A_LD], aiw0[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int m = m0 + (tid >> 3) + (NT / 8) * i;
+    const bool v = m < M;
+    const int mm = v ? m : 0;
+    const int ow = mm % a.Wo;
+    const int t2 = mm / a.Wo;
+    const int oh = t2 % a.Ho;
+    const int n = t2 / a.Ho;
+    arow[i] = n * (int)a.in_sn;
+    aih0[i] = v ? oh * a.stride - a.pad : -(1 << 28);
+    aiw0[i] = ow * a.stride - a.pad;
+  }
+
+  float4 ra[A_LD];
+  uint4 rbh[B_LD], rbl[B_LD];
+  bool overflow = false;
+
+  auto load_chunk = [&](int k0) {
+    if constexpr (CIN32) {
+      // the whole 32-wide chunk lies inside one filter tap: tap / kh / kw are wave-uniform
+      const int tap = k0 / a.Cin;
+      const int ci = k0 - tap * a.Cin + kq * 4;
+      const int kh = tap / a.KW;
+      const int kw = tap - kh * a.KW;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const int ih = aih0[i] + kh, iw = aiw0[i] + kw;
+        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const uint32_t off = ok ? (uint32_t)(arow[i] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB;
+        uint4 u = bload16(rin, off);
+        ra[i] = *reinterpret_cast<float4*>(&u);
+      }
+    } else {
+      const int kk = k0 + kq * 4;
+      const bool kv = kk < K;
+      const int tap = kk / a.Cin;
+      const int ci = kk - tap * a.Cin;
+      const int kh = tap / a.KW;
+      const int kw = tap - kh * a.KW;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const int ih = aih0[i] + kh, iw = aiw0[i] + kw;
+        const bool ok = kv && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const uint32_t off = ok ? (uint32_t)(arow[i] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB;
+        uint4 u = bload16(rin, off);
+        ra[i] = *reinterpret_cast<float4*>(&u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      const int u = tid + NT * j;
+      const int n = n0 + (u >> 2);
+      const int kb = k0 + (u & 3) * 8;
+      const uint32_t off = (n < a.Cout && kb < Kp) ? (uint32_t)(n * ldh + kb) * 2u : kOOB;
+      rbh[j] = bload16(rwh, off);
+      rbl[j] = bload16(rwl, off);
+    }
+  };
+
+  auto store_chunk = [&](int buf) {
+    char* st = lds + buf * STAGE;
+    char* sah = st;
+    char* sal = st + BM * ROWB;
+    char* sbh = st + 2 * BM * ROWB;
+    char* sbl = st + (2 * BM + BN) * ROWB;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int r = (tid >> 3) + (NT / 8) * i;
+      const float4 v = ra[i];
+      overflow |= fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) >= 65504.f;
+      uint2 h, l;
+      split2(v.x, v.y, h.x, l.x);
+      split2(v.z, v.w, h.y, l.y);
+      const int off = r * ROWB + (((kq >> 1) ^ ((r >> 2) & 3)) << 4) + ((kq & 1) << 3);
+      *reinterpret_cast<uint2*>(sah + off) = h;
+      *reinterpret_cast<uint2*>(sal + off) = l;
+    }
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      const int u = tid + NT * j;
+      const int r = u >> 2;
+      const int off = r * ROWB + (((u & 3) ^ ((r >> 2) & 3)) << 4);
+      *reinterpret_cast<uint4*>(sbh + off) = rbh[j];
+      *reinterpret_cast<uint4*>(sbl + off) = rbl[j];
+    }
+  };
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, hh = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // fragment row byte offsets (row part) and swizzle keys, fixed across chunks
+  int a_row_off[TM], a_key[TM], b_row_off[TN], b_key[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = (wm * TM + i) * 32 + li;
+    a_row_off[i] = r * ROWB;
+    a_key[i] = (r >> 2) & 3;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int r = (wn * TN + j) * 32 + li;
+    b_row_off[j] = r * ROWB;
+    b_key[j] = (r >> 2) & 3;
+  }
+
+  const int nk = (K + BK - 1) / BK;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    const bool more = kc + 1 < nk;
+    if (more) load_chunk((kc + 1) * BK);
+    const char* st = lds + cur * STAGE;
+    const char* sah = st;
+    const char* sal = st + BM * ROWB;
+    const char* sbh = st + 2 * BM * ROWB;
+    const char* sbl = st + (2 * BM + BN) * ROWB;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int slot = 2 * s + hh;
+      half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int off = a_row_off[i] + ((slot ^ a_key[i]) << 4);
+        ah[i] = *reinterpret_cast<const half8*>(sah + off);
+        al[i] = *reinterpret_cast<const half8*>(sal + off);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int off = b_row_off[j] + ((slot ^ b_key[j]) << 4);
+        bh[j] = *reinterpret_cast<const half8*>(sbh + off);
+        bl[j] = *reinterpret_cast<const half8*>(sbl + off);
+      }
+      // small terms first, the hi x hi term last (independent accumulators interleaved)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store_chunk(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (overflow && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+
+  // ---- fused epilogue. C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  float scl_v[TN], bias_v[TN];
+  int ncol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    ncol[j] = n0 + (wn * TN + j) * 32 + li;
+    const bool nv = ncol[j] < a.Cout;
+    bias_v[j] = (a.bias && nv) ? a.bias[ncol[j]] : 0.f;
+    scl_v[j] = nv ? a.wsinv[ncol[j]] * a.alpha : 0.f;
+  }
+  const int osh = (int)a.out_sh, osw = (int)a.out_sw;
+  const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mbase = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh;
+      int ow = mbase % a.Wo;
+      int t2 = mbase / a.Wo;
+      int oh = t2 % a.Ho;
+      int n = t2 / a.Ho;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = mbase + e;
+        if (m < M) {
+          float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
+          const float* rrow = res ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if (ncol[j] < a.Cout) {
+              float v = acc[i][j][q * 4 + e] * scl_v[j] + bias_v[j];
+              if (rrow) v += rrow[ncol[j]];
+              if (a.relu) v = fmaxf(v, 0.f);
+              orow[ncol[j]] = v;
+            }
+          }
+        }
+        if (++ow == a.Wo) {
+          ow = 0;
+          if (++oh == a.Ho) {
+            oh = 0;
+            ++n;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN>
+static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  const int ntm = (M + BM - 1) / BM;
+  const int ntn = (a.Cout + BN - 1) / BN;
+  dim3 grid(ntm * ntn, 1, 1);
+  if (a.Cin % BK == 0)
+    hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+  else
+    hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 0>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
+void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
+  if (a.Cin % 4 != 0) throw std::runtime_error("conv_x3: Cin must be a multiple of 4");
+  if ((a.in_sw % 4) || (a.in_sh % 4) || (a.in_sn % 4) || (reinterpret_cast<uintptr_t>(a.in) % 16))
+    throw std::runtime_error("conv_x3: input strides / base must be 16-byte aligned");
+  if (!a.wh || !a.wl || !a.wsinv) throw std::runtime_error("conv_x3: missing split weights");
+  if ((a.ldh % 8) || (reinterpret_cast<uintptr_t>(a.wh) % 16) || (reinterpret_cast<uintptr_t>(a.wl) % 16))
+    throw std::runtime_error("conv_x3: split weight rows must be 16-byte aligned");
+  if (a.batch != 1 || a.b_kn) throw std::runtime_error("conv_x3: batched / KN operands are not supported");
+  const int64_t M64 = (int64_t)a.Nimg * a.Ho * a.Wo;
+  if (M64 >= (int64_t(1) << 31)) throw std::runtime_error("conv_x3: M too large");
+  const int M = (int)M64;
+  const int K = a.KH * a.KW * a.Cin;
+  if (a.ldh < K) throw std::runtime_error("conv_x3: ldh < K");
+  if (M == 0 || a.Cout == 0) return;
+  const int64_t in_extent = (int64_t)(a.Nimg - 1) * a.in_sn + (int64_t)(a.H - 1) * a.in_sh +
+                            (int64_t)(a.W - 1) * a.in_sw + a.Cin;
+  if (in_extent * 4 >= (int64_t)kOOB || (int64_t)a.Cout * a.ldh * 2 >= (int64_t)kOOB)
+    throw std::runtime_error("conv_x3: operand extent >= 2 GiB (split the batch)");
+  if ((int64_t)a.Ho * a.out_sh >= (int64_t(1) << 31) || (int64_t)a.Ho * a.res_sh >= (int64_t(1) << 31))
+    throw std::runtime_error("conv_x3: per-image output extent too large");
+  const int64_t t128 = ((M + 127) / 128) * (int64_t)((a.Cout + 127) / 128);
+  if (a.Cout <= 64) {
+    if ((M + 255) / 256 >= 256)
+      launch_x3_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64
+    else
+      launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
+  } else if (t128 >= 512) {
+    launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);    // 128 x 128
+  } else if (t128 * 4 >= 512) {
+    launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);    // 64 x 64
+  } else {
+    launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);
+  }
+}
+
+}  // namespace ddmi

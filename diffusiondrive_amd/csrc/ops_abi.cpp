@@ -5,6 +5,8 @@
 
 #include "../../include/ddmi.h"
 #include "common.h"
+#include "weights.h"
+#include <vector>
 
 namespace {
 thread_local std::string g_op_err;
@@ -63,6 +65,56 @@ int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt
     a.pad = pad;
     a.relu = relu;
     launch_conv_gemm(a, S(stream));
+  });
+}
+
+int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
+                    const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
+                    unsigned* flags, void* stream) {
+  return op_guard([&] {
+    // split the (device) fp32 weights on the host exactly as dd_create does (weights.cpp:prep_split)
+    const int K = KH * KW * Cin;
+    std::vector<float> hw((size_t)Cout * K);
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));
+    DD_HIP_CHECK(hipMemcpy(hw.data(), wgt, hw.size() * sizeof(float), hipMemcpyDeviceToHost));
+    Arena ar;
+    const SplitW x = prep_split(ar, hw.data(), Cout, K);
+    ar.upload();
+    ConvArgs a;
+    a.in = in;
+    a.in_sw = Cin;
+    a.in_sh = (int64_t)W * Cin;
+    a.in_sn = (int64_t)H * W * Cin;
+    a.H = H;
+    a.W = W;
+    a.Cin = Cin;
+    a.wgt = wgt;
+    a.ldb = K;
+    a.bias = bias;
+    a.Nimg = B;
+    a.Ho = (H + 2 * pad - KH) / stride + 1;
+    a.Wo = (W + 2 * pad - KW) / stride + 1;
+    a.Cout = Cout;
+    a.out = out;
+    a.out_sw = Cout;
+    a.out_sh = (int64_t)a.Wo * Cout;
+    a.out_sn = (int64_t)a.Ho * a.Wo * Cout;
+    a.res = res;
+    a.res_sw = a.out_sw;
+    a.res_sh = a.out_sh;
+    a.res_sn = a.out_sn;
+    a.KH = KH;
+    a.KW = KW;
+    a.stride = stride;
+    a.pad = pad;
+    a.relu = relu;
+    a.wh = reinterpret_cast<const uint16_t*>(ar.ptr(x.hi));
+    a.wl = reinterpret_cast<const uint16_t*>(ar.ptr(x.lo));
+    a.wsinv = ar.ptr(x.sinv);
+    a.ldh = x.ldh;
+    a.flags = flags;
+    launch_conv_gemm(a, S(stream));
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));  // the split images die with `ar`
   });
 }
 

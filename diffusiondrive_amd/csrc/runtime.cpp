@@ -111,6 +111,8 @@ class Model {
   std::map<std::string, std::pair<float*, size_t>> bufs;
   bool profiling = false;
   bool use_graph = true;
+  int gemm_mode = DD_GEMM_FP32;       // DD_GEMM_FP32 | DD_GEMM_F16X3 (dd_set_gemm_mode)
+  unsigned* num_flags = nullptr;      // device word: DD_NUM_* bits raised by kernels
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;
   std::map<std::string, KStat> stats;
@@ -132,6 +134,13 @@ class Model {
     ar.upload();
     decoder_init_constants();
     DD_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
+    DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
+    if (const char* g = getenv("DDMI_GEMM")) {
+      if (!strcmp(g, "fp32")) gemm_mode = DD_GEMM_FP32;
+      else if (!strcmp(g, "f16x3")) gemm_mode = DD_GEMM_F16X3;
+      else throw std::invalid_argument(std::string("DDMI_GEMM must be fp32 or f16x3, got ") + g);
+    }
     DD_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     DD_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     // diffusers DDIMScheduler(beta_schedule="scaled_linear") schedule, bit-exact to the float32
@@ -161,6 +170,7 @@ class Model {
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (st) (void)hipStreamDestroy(st);
+    if (num_flags) (void)hipFree(num_flags);
     for (auto& kv : bufs) (void)hipFree(kv.second.first);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& p : pending) {
@@ -216,6 +226,7 @@ class Model {
     }
     Lin l;
     l.w = ar.add(w);
+    l.x3 = prep_split(ar, w.data(), 3 * C, C);
     l.b = ar.add(b);
     l.nout = 3 * C;
     l.nin = C;
@@ -389,6 +400,16 @@ class Model {
     if (log) fclose(log);
   }
 
+  // route a conv / linear to the f16x3 split-MFMA kernel when that mode is on
+  void use_split(ConvArgs& a, const SplitW& x) {
+    if (gemm_mode != DD_GEMM_F16X3 || x.hi == kNone) return;
+    a.wh = reinterpret_cast<const uint16_t*>(W(x.hi));
+    a.wl = reinterpret_cast<const uint16_t*>(W(x.lo));
+    a.wsinv = W(x.sinv);
+    a.ldh = x.ldh;
+    a.flags = num_flags;
+  }
+
   // conv on strided NHWC views
   void conv(const Conv& c, const float* in, int64_t isn, int64_t ish, int64_t isw, int N, int H, int Wd, float* out,
             int64_t osn, int64_t osh, int64_t osw, bool relu, const float* res = nullptr, int64_t rsn = 0,
@@ -420,6 +441,7 @@ class Model {
     a.stride = c.stride;
     a.pad = c.pad;
     a.relu = relu;
+    use_split(a, c.x3);
     const double fl = 2.0 * N * a.Ho * a.Wo * (double)c.cout * c.k * c.k * c.cin_real;
     launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
@@ -461,6 +483,7 @@ class Model {
     a.Wo = 1;
     a.Cout = L.nout;
     a.relu = relu;
+    use_split(a, L.x3);
     const double fl = 2.0 * G * R * (double)L.nout * L.nin;
     launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
@@ -902,7 +925,8 @@ class Model {
     const uint64_t gen0 = generation;
     stage_inputs(camera, lidar, status, noise, B);
     if (generation != gen0) known_shapes.clear();
-    const std::string key = std::to_string(B) + "/" + std::to_string(steps) + "/" + std::to_string(heads);
+    const std::string key = std::to_string(B) + "/" + std::to_string(steps) + "/" + std::to_string(heads) + "/g" +
+                            std::to_string(gemm_mode);
     if (use_graph && !profiling && known_shapes.count(key)) {
       const std::string gkey = key + "#" + std::to_string(generation);
       if (graph.key != gkey) {
@@ -1053,6 +1077,34 @@ int dd_set_graph(dd_handle* h, int enable) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
     h->m->use_graph = enable != 0;
+  });
+}
+
+int dd_set_gemm_mode(dd_handle* h, int mode) {
+  return guarded([&] {
+    if (!h) throw std::invalid_argument("null handle");
+    if (mode != DD_GEMM_FP32 && mode != DD_GEMM_F16X3) throw std::invalid_argument("unknown gemm mode");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->m->gemm_mode = mode;
+  });
+}
+
+int dd_get_gemm_mode(dd_handle* h, int* mode) {
+  return guarded([&] {
+    if (!h || !mode) throw std::invalid_argument("null argument");
+    *mode = h->m->gemm_mode;
+  });
+}
+
+int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear) {
+  return guarded([&] {
+    if (!h || !flags) throw std::invalid_argument("null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    Model& m = *h->m;
+    DD_HIP_CHECK(hipSetDevice(m.device));
+    DD_HIP_CHECK(hipStreamSynchronize(m.st));
+    DD_HIP_CHECK(hipMemcpy(flags, m.num_flags, sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (clear) DD_HIP_CHECK(hipMemset(m.num_flags, 0, sizeof(unsigned)));
   });
 }
 

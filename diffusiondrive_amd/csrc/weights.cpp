@@ -8,6 +8,7 @@
 // transfuser_agent.py:94-106).
 #include "weights.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -94,6 +95,47 @@ size_t Arena::add(const float* data, size_t n) {
 
 size_t Arena::add(const std::vector<float>& v) { return add(v.data(), v.size()); }
 
+size_t Arena::add_zero(size_t n) {
+  size_t off = host_.size();
+  host_.resize(off + n, 0.f);
+  host_.resize((host_.size() + 15) & ~size_t(15), 0.f);
+  return off;
+}
+
+// f16x3 weight split (conv_x3.hip header): per row r, s_r = 2^e with max|w_r| * s_r in
+// [2^14, 2^15] (exact power-of-two scaling, no fp16 overflow, lo parts clear of the subnormal
+// range); hi = f16(w * s_r), lo = f16(w * s_r - hi), both RNE; sinv[r] = 1 / s_r.
+SplitW prep_split(Arena& ar, const float* w, int rows, int K) {
+  SplitW x;
+  x.ldh = (K + 7) / 8 * 8;
+  const size_t nh = (size_t)rows * x.ldh;  // halfs per image
+  x.hi = ar.add_zero((nh + 1) / 2);
+  x.lo = ar.add_zero((nh + 1) / 2);
+  std::vector<float> sinv(rows, 1.f);
+  _Float16* hi = reinterpret_cast<_Float16*>(ar.host(x.hi));
+  _Float16* lo = reinterpret_cast<_Float16*>(ar.host(x.lo));
+  for (int r = 0; r < rows; ++r) {
+    float amax = 0.f;
+    for (int k = 0; k < K; ++k) amax = std::max(amax, std::fabs(w[(size_t)r * K + k]));
+    int e = 0;
+    if (amax > 0.f && std::isfinite(amax)) {
+      int ex;
+      std::frexp(amax, &ex);  // amax = f * 2^ex, f in [0.5, 1)
+      e = 15 - ex;            // amax * 2^e in [2^14, 2^15)
+    }
+    const float s = std::ldexp(1.0f, e);
+    sinv[r] = std::ldexp(1.0f, -e);
+    for (int k = 0; k < K; ++k) {
+      const float v = w[(size_t)r * K + k] * s;
+      const _Float16 h = (_Float16)v;
+      hi[(size_t)r * x.ldh + k] = h;
+      lo[(size_t)r * x.ldh + k] = (_Float16)(v - (float)h);
+    }
+  }
+  x.sinv = ar.add(sinv);
+  return x;
+}
+
 void Arena::upload() {
   if (dev_) DD_HIP_CHECK(hipFree(dev_));
   DD_HIP_CHECK(hipMalloc(&dev_, std::max<size_t>(host_.size(), 16) * sizeof(float)));
@@ -136,6 +178,7 @@ Conv prep_conv(const BlobIndex& bx, Arena& ar, const std::string& wname, int cou
   bool any_bias = !bn_prefix.empty() || !bias_name.empty();
   for (int o = 0; o < cout; ++o) bl[o] = (float)shift[o];
   Conv c;
+  c.x3 = prep_split(ar, wl.data(), cout, k * k * cin_p);
   c.w = ar.add(wl);
   c.b = any_bias ? ar.add(bl) : kNone;
   c.cout = cout;
@@ -151,6 +194,7 @@ Lin prep_linear(const BlobIndex& bx, Arena& ar, const std::string& prefix, int n
   const HostTensor& w = bx.get(prefix + ".weight", {nout, nin});
   Lin l;
   l.w = ar.add(w.data, w.numel);
+  l.x3 = prep_split(ar, w.data, nout, nin);
   l.b = bias ? ar.add(bx.get(prefix + ".bias", {nout}).data, (size_t)nout) : kNone;
   l.nout = nout;
   l.nin = nin;
@@ -163,6 +207,7 @@ Lin prep_linear_rows(const BlobIndex& bx, Arena& ar, const std::string& wname, c
   const HostTensor& b = bx.get(bname, {rows_total});
   Lin l;
   l.w = ar.add(w.data + (size_t)row0 * nin, (size_t)nrows * nin);
+  l.x3 = prep_split(ar, w.data + (size_t)row0 * nin, nrows, nin);
   l.b = ar.add(b.data + row0, (size_t)nrows);
   l.nout = nrows;
   l.nin = nin;

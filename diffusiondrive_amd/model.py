@@ -170,6 +170,25 @@ class DiffusionDriveModel:
                                    torch.cuda.current_stream(self.device).cuda_stream), self.lib)
         return t if shape is None else t[: int(np.prod(shape))].view(*shape)
 
+    GEMM_MODES = {"fp32": 0, "f16x3": 1}
+
+    def set_gemm_mode(self, mode: str):
+        """'fp32' (fp32-input MFMA) or 'f16x3' (3-product fp16 split MFMA; include/ddmi.h)."""
+        if mode not in self.GEMM_MODES:
+            raise ValueError(f"gemm mode must be one of {sorted(self.GEMM_MODES)}, got {mode!r}")
+        _lib.check(self.lib.dd_set_gemm_mode(self.handle, self.GEMM_MODES[mode]), self.lib)
+
+    def gemm_mode(self) -> str:
+        m = ctypes.c_int()
+        _lib.check(self.lib.dd_get_gemm_mode(self.handle, ctypes.byref(m)), self.lib)
+        return {v: k for k, v in self.GEMM_MODES.items()}[m.value]
+
+    def numerics_flags(self, clear: bool = True) -> int:
+        """DD_NUM_* bits raised since the last clear (bit 0: f16x3 activation overflow)."""
+        f = ctypes.c_uint()
+        _lib.check(self.lib.dd_numerics_flags(self.handle, ctypes.byref(f), int(clear)), self.lib)
+        return f.value
+
     def set_profiling(self, on: bool):
         _lib.check(self.lib.dd_set_profiling(self.handle, int(on)), self.lib)
 

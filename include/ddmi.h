@@ -93,6 +93,21 @@ int dd_reset_stats(dd_handle* h);
 int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long long* launches, double* flops);
 /* Enable / disable hipGraph capture + replay of the forward (default on). */
 int dd_set_graph(dd_handle* h, int enable);
+/* GEMM arithmetic of every conv / linear of the path:
+ *   DD_GEMM_FP32   fp32-input MFMA (v_mfma_f32_32x32x2_f32), an exact fp32 fma chain;
+ *   DD_GEMM_F16X3  3-product fp16 split on f16 MFMA (conv_x3.hip): each fp32 operand becomes
+ *                  hi + lo fp16, products ah*bh + ah*bl + al*bh accumulate in fp32 - fp32-class
+ *                  accuracy (<= ~3*2^-22 relative per product) at 5.3x the fp32 MFMA rate.
+ * Default DD_GEMM_FP32, or $DDMI_GEMM=fp32|f16x3 at dd_create. Attention score GEMMs stay fp32. */
+#define DD_GEMM_FP32 0
+#define DD_GEMM_F16X3 1
+int dd_set_gemm_mode(dd_handle* h, int mode);
+int dd_get_gemm_mode(dd_handle* h, int* mode);
+/* Numerics flags raised by kernels since the last clear (synchronises the handle's stream):
+ * bit 0 (DD_NUM_F16_OVERFLOW_BIT) = an activation reached |x| >= 65504 under DD_GEMM_F16X3, so that
+ * forward's result is not trustworthy (re-run it in DD_GEMM_FP32). clear != 0 resets them. */
+#define DD_NUM_F16_OVERFLOW_BIT 1u
+int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear);
 /* Copy a named internal buffer (e.g. "p3", "keyval", "cross_bev", "reg_s0l1") of the last
  * forward into dst (device pointer), at most `count` floats; *actual = buffer length. */
 int dd_tap(dd_handle* h, const char* name, float* dst, size_t count, size_t* actual, void* stream);
@@ -103,6 +118,11 @@ const char* dd_op_last_error(void);
 /* NHWC conv: in (B,H,W,Cin), wgt (Cout,KH,KW,Cin), optional bias (Cout), res (B,Ho,Wo,Cout). */
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
                  const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream);
+/* Same conv on the f16x3 split kernel (weights split on the host as dd_create does; synchronous).
+ * flags (device unsigned, nullable) receives DD_NUM_F16_OVERFLOW_BIT. */
+int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
+                    const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
+                    unsigned* flags, void* stream);
 /* C (M,N) = A (M,K) . W(N,K)^T [+ bias] [+ res (M,N)] [relu] */
 int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,
                int relu, void* stream);

@@ -69,6 +69,53 @@ def test_conv2d(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     close(out.permute(0, 3, 1, 2), ref, 2e-5)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p,relu,res", [
+    (2, 16, 24, 64, 64, 3, 1, 1, True, True),     # BasicBlock conv2 (+residual), Cin % 32 == 0 path
+    (2, 16, 24, 64, 128, 3, 2, 1, True, False),   # stage-entry conv1 (stride 2)
+    (2, 16, 24, 64, 128, 1, 2, 0, False, False),  # downsample 1x1/s2
+    (1, 40, 70, 4, 64, 7, 2, 3, True, False),     # stem (3 -> padded 4 channels), generic K path
+    (2, 8, 8, 512, 7, 1, 1, 0, False, False),     # tiny Cout
+    (1, 64, 64, 256, 256, 3, 1, 1, True, False),  # value_proj
+    (3, 5, 7, 320, 40, 1, 1, 0, True, True),      # ragged M / N
+    (2, 64, 80, 64, 64, 3, 1, 1, True, False),    # Cout 64, 256-row tiles
+    (1, 48, 64, 128, 256, 3, 1, 1, False, True),  # 128x128 tiles
+    (1, 9, 11, 36, 24, 3, 1, 1, False, False),    # Cin % 32 != 0, K tail
+])
+def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
+    """f16x3 split-MFMA conv vs PyTorch-CPU fp32 (tolerance: fp32-class, 3e-5 of max|ref|)."""
+    x = rnd(B, Cin, H, W, seed=11)
+    w = rnd(Cout, Cin, k, k, seed=12, scale=1.0 / np.sqrt(Cin * k * k))
+    b = rnd(Cout, seed=13)
+    ref = F.conv2d(x.double(), w.double(), b.double(), s, p)
+    r = rnd(*ref.shape, seed=14) if res else None
+    if res:
+        ref = ref + r.double()
+    if relu:
+        ref = F.relu(ref)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win, bin_ = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b)
+    rin = g(r.permute(0, 2, 3, 1)) if res else None
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(),
+                           rin.data_ptr() if res else None, out.data_ptr(), Cout, k, k, s, p, int(relu),
+                           flags.data_ptr(), None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 3e-5)
+    assert int(flags.item()) == 0
+
+
+def test_conv2d_f16x3_flags_overflow(gpu):
+    """An activation beyond the fp16 range must raise DD_NUM_F16_OVERFLOW_BIT (never pass silently)."""
+    x = rnd(1, 32, 8, 8, seed=15)
+    x[0, 3, 2, 2] = 1e6
+    w = rnd(32, 32, 1, 1, seed=16)
+    out = torch.empty(1, 8, 8, 32, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), 1, 8, 8, 32, win.data_ptr(), None, None, out.data_ptr(), 32, 1, 1, 1, 0,
+                           0, flags.data_ptr(), None), gpu)
+    assert int(flags.item()) & 1
+
+
 @pytest.mark.parametrize("M,K,N,relu", [(1, 256, 1024, False), (1280, 256, 256, True), (4096, 320, 256, True),
                                         (600, 1024, 24, False), (77, 8, 256, False), (1280, 256, 1, False)])
 def test_gemm(gpu, M, K, N, relu):

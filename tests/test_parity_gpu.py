@@ -32,16 +32,21 @@ def _report(lines):
     print("\n".join(lines))
 
 
+GEMM_MODES = ["fp32", "f16x3"]
+
+
+@pytest.mark.parametrize("mode", GEMM_MODES)
 @pytest.mark.parametrize("path", golden_files(), ids=os.path.basename)
-def test_forward_matches_reference_goldens(gpu_model, path):
+def test_forward_matches_reference_goldens(gpu_model, path, mode):
     from diffusiondrive_amd.weights import synthetic_inputs
+    gpu_model.set_gemm_mode(mode)
     g = load(path)
     B, seed = int(g["batch"]), int(g["seed"])
     inp = synthetic_inputs(B, seed)
     assert np.array_equal(inp["noise"], g["noise"])
     feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
     out = gpu_model.forward(feats, noise=torch.from_numpy(inp["noise"]), heads=True, modes=True)
-    lines = [f"== {os.path.basename(path)} B={B}"]
+    lines = [f"== {os.path.basename(path)} B={B} gemm={mode}"]
     l2 = waypoint_l2(out["trajectory"].numpy(), g["trajectory"])
     hd = float(np.abs(out["trajectory"].numpy()[..., 2] - g["trajectory"][..., 2]).max())
     lines.append(f"trajectory: waypoint L2 max {l2:.3e}  heading max {hd:.3e}")
@@ -73,6 +78,7 @@ def test_forward_matches_reference_goldens(gpu_model, path):
     for k, (e, cs) in tap_errs.items():
         lines.append(f"  tap {k:18s} sample rel err {e:.3e}  checksum rel err {cs:.3e}")
     _report(lines)
+    assert gpu_model.numerics_flags() == 0
     assert l2 <= WAYPOINT_L2_TOL, f"waypoint L2 {l2:.3e} > {WAYPOINT_L2_TOL}"
     assert hd <= HEADING_TOL
     for k, v in errs.items():
@@ -81,9 +87,11 @@ def test_forward_matches_reference_goldens(gpu_model, path):
         assert e <= TAP_TOL and cs <= TAP_TOL, (k, e, cs)
 
 
-def test_forward_graph_replay_is_deterministic(gpu_model):
+@pytest.mark.parametrize("mode", GEMM_MODES)
+def test_forward_graph_replay_is_deterministic(gpu_model, mode):
     """Second and third calls replay the captured hipGraph: results must be bit-identical."""
     from diffusiondrive_amd.weights import synthetic_inputs
+    gpu_model.set_gemm_mode(mode)
     inp = synthetic_inputs(2, 99)
     feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
     nz = torch.from_numpy(inp["noise"])
@@ -93,9 +101,11 @@ def test_forward_graph_replay_is_deterministic(gpu_model):
     assert torch.equal(a, b) and torch.equal(b, c)
 
 
-def test_forward_matches_oracle_batch8(gpu_model, seeded_sd):
+@pytest.mark.parametrize("mode", GEMM_MODES)
+def test_forward_matches_oracle_batch8(gpu_model, seeded_sd, mode):
     """Wider check vs the golden-pinned CPU oracle on an unseen seed (B=8)."""
     from oracle.model import OracleModel
+    gpu_model.set_gemm_mode(mode)
     from diffusiondrive_amd.weights import synthetic_inputs
     inp = synthetic_inputs(8, 4321)
     ref = OracleModel(seeded_sd).forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"],
@@ -103,6 +113,7 @@ def test_forward_matches_oracle_batch8(gpu_model, seeded_sd):
     feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
     out = gpu_model.forward(feats, noise=torch.from_numpy(inp["noise"]), modes=True)
     l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
-    _report([f"== oracle B=8 seed 4321: waypoint L2 {l2:.3e}, "
+    _report([f"== oracle B=8 seed 4321 gemm={mode}: waypoint L2 {l2:.3e}, "
              f"modes max err {float((out['poses_reg'] - ref['poses_reg']).abs().max()):.3e}"])
+    assert gpu_model.numerics_flags() == 0
     assert l2 <= WAYPOINT_L2_TOL

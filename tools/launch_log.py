@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--arch", default="resnet34")
+    ap.add_argument("--gemm", default="fp32")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "launches.md"))
     a = ap.parse_args()
     log = tempfile.NamedTemporaryFile(prefix="ddmi_launch_", suffix=".tsv", delete=False).name
@@ -35,6 +36,7 @@ def main():
 
     cfg = TransfuserConfig(image_architecture=a.arch)
     model = DiffusionDriveModel(cfg, seeded_state_dict(cfg, 0), device=0)
+    model.set_gemm_mode(a.gemm)
     inp = synthetic_inputs(a.batch, 1234, cfg)
     feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
     noise = torch.from_numpy(inp["noise"]).cuda()
@@ -63,7 +65,7 @@ def main():
             g[1] += float(flops) / a.reps
             g[2] += ms
     rows = sorted(groups.items(), key=lambda kv: -kv[1][2])
-    lines = [f"# conv_gemm launches per forward (B={a.batch}, {a.arch}); forward device total {total:.2f} ms", "",
+    lines = [f"# conv_gemm launches per forward (B={a.batch}, {a.arch}, gemm={a.gemm}); forward device total {total:.2f} ms", "",
              "| shape | launches | ms | GFLOP | TFLOP/s | frac fp32 peak | share |", "|---|---|---|---|---|---|---|"]
     cg_ms = sum(v[2] for _, v in rows)
     cg_fl = sum(v[1] for _, v in rows)
