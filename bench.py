@@ -30,6 +30,17 @@ import torch  # noqa: E402
 
 CANONICAL_GFLOP_PER_SCENE_2STEP = 65.27  # SURVEY.md §8d (value_proj once per layer)
 FP32_MFMA_PEAK_TFLOPS = 157.3            # MI355X dense fp32 MFMA (= vector) peak
+F16_MFMA_PEAK_TFLOPS = 2500.0            # MI355X dense f16 MFMA peak (no sparsity)
+# peak of ALGORITHMIC fp32 FLOPs per gemm mode: f16x3 issues 3 f16 MFMA products per fp32 MAC
+ALGO_PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16x3": F16_MFMA_PEAK_TFLOPS / 3}
+KERNEL_DESC = {
+    "fp32": "conv_gemm (implicit-GEMM conv / GEMM, fp32 MFMA v_mfma_f32_32x32x2_f32)",
+    "f16x3": "conv_x3 (implicit-GEMM conv / GEMM, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
+}
+DTYPE = {
+    "fp32": "fp32",
+    "f16x3": "fp32 via f16x3 (each fp32 operand = hi+lo fp16, products ah*bh+ah*bl+al*bh, fp32 accumulate)",
+}
 
 
 def parse():
@@ -43,8 +54,9 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--arch", default="resnet34")
-    p.add_argument("--gemm", default="fp32", choices=["fp32", "f16x3"],
+    p.add_argument("--gemm", default="f16x3", choices=["fp32", "f16x3"],
                    help="conv/linear arithmetic: fp32 MFMA or the fp32-class 3-product fp16 split")
+    p.add_argument("--no-compare", action="store_true", help="skip the fp32-path comparison timing")
     return p.parse_args()
 
 
@@ -102,6 +114,10 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     scenes_per_s = B * world * args.steps / elapsed
     traj_gpu = out[rank * B:(rank + 1) * B].detach().cpu().numpy()
+    num_flags = model.numerics_flags()
+    if num_flags:
+        print(f"[bench] WARNING: numerics flags {num_flags:#x} raised (f16x3 overflow): result untrustworthy",
+              file=sys.stderr)
 
     # ---- roofline of the dominant kernel: a profiled replay of the same workload (HIP events
     # around every conv_gemm launch on the handle's stream)
@@ -111,17 +127,37 @@ def main():
     for _ in range(prof_steps):
         model.forward(feats, noise=noise, steps=args.denoise_steps)
     torch.cuda.synchronize()
-    st = model.kernel_stats("conv_gemm")
-    other = {k: model.kernel_stats(k) for k in ("layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
-                                                 "misc")}
+    main_k = "conv_x3" if args.gemm == "f16x3" else "conv_gemm"
+    st = model.kernel_stats(main_k)
+    other = {k: model.kernel_stats(k) for k in ("conv_gemm", "layernorm", "softmax", "bilinear", "pool", "mha",
+                                                 "bev_sample", "misc") if k != main_k}
     model.set_profiling(False)
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["flops"] / max(st["launches"], 1)
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     total_prof_ms = st["ms"] + sum(v["ms"] for v in other.values())
 
+    # the other gemm mode on the same workload, for comparison (rank 0 view, N = 1 only)
+    compare = None
+    if world == 1 and not args.no_compare:
+        other_mode = "fp32" if args.gemm == "f16x3" else "f16x3"
+        model.set_gemm_mode(other_mode)
+        for _ in range(2):
+            o2 = step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_cmp = max(3, args.steps // 2)
+        for _ in range(n_cmp):
+            o2 = step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        d = (o2.detach().cpu().numpy()[..., :2].astype(np.float64) - traj_gpu[..., :2]).reshape(B, -1)
+        compare = {"gemm": other_mode, "value": round(B * n_cmp / dt, 3), "ms_per_step": round(dt / n_cmp * 1e3, 3),
+                   "steps": n_cmp, "waypoint_l2_vs_primary": float(np.sqrt((d ** 2).sum(-1)).max())}
+        model.set_gemm_mode(args.gemm)
+
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_conv_gemm.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_conv_gemm_{args.gemm}.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
@@ -140,7 +176,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": DTYPE[args.gemm],
         "data": "synthetic (seeded camera/LiDAR/status/noise; seeded random weights of the reference architecture)",
         "config": {
             "workload": f"DiffusionDrive eval forward: {args.arch} camera + ResNet-34 LiDAR-BEV backbone, "
@@ -151,14 +187,18 @@ def main():
             "denoise_steps": args.denoise_steps,
             "parallelism": f"dp{world} (scene sharding, RCCL all_gather of trajectories)",
             "graph": True,
+            "gemm": args.gemm,
         },
         "roofline": {
-            "kernel": "conv_gemm (implicit-GEMM conv / GEMM, fp32 MFMA 32x32x2)",
+            "kernel": KERNEL_DESC[args.gemm],
             "bound": "mfma",
             "achieved": round(achieved, 3),
-            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "peak": round(ALGO_PEAK[args.gemm], 1),
             "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "frac": round(achieved / ALGO_PEAK[args.gemm], 4),
+            "peak_note": "algorithmic fp32 FLOP/s ceiling: fp32 MFMA 157.3 TF" if args.gemm == "fp32" else
+                         "algorithmic fp32 FLOP/s ceiling: dense f16 MFMA 2500 TF / 3 products per fp32 MAC",
+            "achieved_vs_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
             "traffic": traffic,
             "launches_per_step": st["launches"] // prof_steps,
             "avg_launch_ms": round(avg_ms, 5),
@@ -175,6 +215,9 @@ def main():
         result["whole_forward"]["frac_of_fp32_peak"] = round(result["whole_forward"]["tflops"] / FP32_MFMA_PEAK_TFLOPS,
                                                              4)
 
+    result["numerics_flags"] = num_flags
+    if compare is not None:
+        result["compare_gemm_mode"] = compare
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, cfg, sd, inp, traj_gpu)
     if rank == 0:

@@ -12,9 +12,9 @@
 //
 // Range: weights are pre-split on the host with a per-output-channel power-of-two scale that puts
 // max|w| at 2^15 (exact; undone in the epilogue), so no weight lo part is lost to fp16 subnormals.
-// Activations are split unscaled: an |x| >= 65504 would overflow fp16, so the kernel ORs
-// DD_NUM_F16_OVERFLOW into *flags (the runtime reports it via dd_numerics_flags; the host agent
-// raises / re-runs in fp32). Activations below 2^-3 have a subnormal lo part: absolute error
+// Activations are split unscaled: an |x| >= 65504 overflows its fp16 hi part, which makes every
+// output it feeds non-finite; the epilogue ORs DD_NUM_F16_OVERFLOW into *flags for any non-finite
+// accumulator (the runtime reports it via dd_numerics_flags; the host raises / re-runs in fp32). Activations below 2^-3 have a subnormal lo part: absolute error
 // <= 2^-25, negligible against the row sums it feeds.
 //
 // Tiling (MI355X-first):
@@ -28,6 +28,9 @@
 //  * Double-buffered LDS; chunk k+1's global loads are in flight during chunk k's MFMAs.
 //  * XCD-aware bijective tile remap (blocks b, b+8, ... share an XCD's L2 -> consecutive tiles).
 //  * Fused epilogue: per-channel weight scale, alpha, bias, residual, ReLU, strided NHWC store.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 
 namespace ddmi {
@@ -35,6 +38,8 @@ namespace ddmi {
 namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
@@ -49,19 +54,14 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return *reinterpret_cast<uint4*>(&v);
 }
 
-// fp32 -> (hi, lo) fp16 pair, packed 2 per dword.
-__device__ inline void split2(float x, float y, uint32_t& hi, uint32_t& lo) {
-  const _Float16 hx = (_Float16)x, hy = (_Float16)y;
-  const _Float16 lx = (_Float16)(x - (float)hx), ly = (_Float16)(y - (float)hy);
-  hi = (uint32_t)__builtin_bit_cast(uint16_t, hx) | ((uint32_t)__builtin_bit_cast(uint16_t, hy) << 16);
-  lo = (uint32_t)__builtin_bit_cast(uint16_t, lx) | ((uint32_t)__builtin_bit_cast(uint16_t, ly) << 16);
-}
-
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int CIN32>
+template <int WM, int WN, int TM, int TN, int MODE>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
+  // MODE 1: Cin % 32 == 0 and KH*KW <= 32 - a 32-wide K chunk lies inside one filter tap, the
+  //         tap walk is scalar and each A row carries a precomputed base offset + tap-valid mask;
+  // MODE 0: generic K (stem 7x7 on 4 padded channels, small Cin): per-lane tap decode.
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
@@ -86,10 +86,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   const int m0 = mt_idx * BM;
   const int n0 = nt_idx * BN;
 
-  const float* in = a.in;
-  float* out = a.out;
-  const float* res = a.res;
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(in);
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in);
   const __amdgpu_buffer_rsrc_t rwh = make_rsrc(a.wh);
   const __amdgpu_buffer_rsrc_t rwl = make_rsrc(a.wl);
   const int in_sh = (int)a.in_sh, in_sw = (int)a.in_sw;
@@ -98,7 +95,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
 
   // ---- per-thread A rows (fixed across K chunks)
   const int kq = tid & 7;  // float4 index inside the 32-wide K chunk
-  int arow[A_LD], aih0[A_LD], aiw0[A_LD];
+  int abase[A_LD], aih0[A_LD], aiw0[A_LD];
+  uint32_t amask[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = m0 + (tid >> 3) + (NT / 8) * i;
@@ -108,29 +106,60 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     const int t2 = mm / a.Wo;
     const int oh = t2 % a.Ho;
     const int n = t2 / a.Ho;
-    arow[i] = n * (int)a.in_sn;
-    aih0[i] = v ? oh * a.stride - a.pad : -(1 << 28);
-    aiw0[i] = ow * a.stride - a.pad;
+    const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+    if constexpr (MODE == 1) {
+      // element offset of tap (0, 0) channel kq*4, and bit t set iff tap t reads inside the image
+      abase[i] = n * (int)a.in_sn + ih0 * in_sh + iw0 * in_sw + kq * 4;
+      uint32_t mk = 0;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+            mk |= 1u << (kh * a.KW + kw);
+      amask[i] = v ? mk : 0u;
+    } else {
+      abase[i] = n * (int)a.in_sn;
+      aih0[i] = v ? ih0 : -(1 << 28);
+      aiw0[i] = iw0;
+    }
+  }
+  // B rows: constant part of the byte offset and validity
+  uint32_t boff[B_LD];
+  bool bok[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int u = tid + NT * j;
+    const int n = n0 + (u >> 2);
+    bok[j] = n < a.Cout;
+    boff[j] = (uint32_t)(n * ldh + (u & 3) * 8) * 2u;
   }
 
-  float4 ra[A_LD];
-  uint4 rbh[B_LD], rbl[B_LD];
-  bool overflow = false;
+  // two register staging sets: chunk c lives in set c % 2 (global loads run two chunks ahead)
+  float4 ra[2][A_LD];
+  uint4 rbh[2][B_LD], rbl[2][B_LD];
+  // scalar tap walk (MODE 1): the chunk at k0 reads channels ci0 .. ci0+31 of tap (kh, kw)
+  int t_tap = 0, t_ci = 0, t_kw = 0, t_off = 0;
 
-  auto load_chunk = [&](int k0) {
-    if constexpr (CIN32) {
-      // the whole 32-wide chunk lies inside one filter tap: tap / kh / kw are wave-uniform
-      const int tap = k0 / a.Cin;
-      const int ci = k0 - tap * a.Cin + kq * 4;
-      const int kh = tap / a.KW;
-      const int kw = tap - kh * a.KW;
+  auto load_chunk = [&](auto SET, int k0) {
+    constexpr int S = decltype(SET)::value;
+    if constexpr (MODE == 1) {
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
-        const int ih = aih0[i] + kh, iw = aiw0[i] + kw;
-        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        const uint32_t off = ok ? (uint32_t)(arow[i] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB;
+        const bool ok = t_tap < 32 && ((amask[i] >> (t_tap & 31)) & 1u);
+        const uint32_t off = ok ? (uint32_t)(abase[i] + t_off) * 4u : kOOB;
         uint4 u = bload16(rin, off);
-        ra[i] = *reinterpret_cast<float4*>(&u);
+        ra[S][i] = *reinterpret_cast<float4*>(&u);
+      }
+      // advance the walk by 32 channels (wave-uniform: SALU)
+      t_ci += BK;
+      t_off += BK;
+      if (t_ci == a.Cin) {
+        t_ci = 0;
+        ++t_tap;
+        t_off += in_sw - a.Cin;
+        if (++t_kw == a.KW) {
+          t_kw = 0;
+          t_off += in_sh - a.KW * in_sw;
+        }
       }
     } else {
       const int kk = k0 + kq * 4;
@@ -143,23 +172,36 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
       for (int i = 0; i < A_LD; ++i) {
         const int ih = aih0[i] + kh, iw = aiw0[i] + kw;
         const bool ok = kv && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        const uint32_t off = ok ? (uint32_t)(arow[i] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB;
+        const uint32_t off = ok ? (uint32_t)(abase[i] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB;
         uint4 u = bload16(rin, off);
-        ra[i] = *reinterpret_cast<float4*>(&u);
+        ra[S][i] = *reinterpret_cast<float4*>(&u);
       }
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      const int u = tid + NT * j;
-      const int n = n0 + (u >> 2);
-      const int kb = k0 + (u & 3) * 8;
-      const uint32_t off = (n < a.Cout && kb < Kp) ? (uint32_t)(n * ldh + kb) * 2u : kOOB;
-      rbh[j] = bload16(rwh, off);
-      rbl[j] = bload16(rwl, off);
+      const int kb = k0 + ((tid + NT * j) & 3) * 8;
+      const uint32_t off = (bok[j] && kb < Kp) ? boff[j] + (uint32_t)k0 * 2u : kOOB;
+      rbh[S][j] = bload16(rwh, off);
+      rbl[S][j] = bload16(rwl, off);
     }
   };
 
-  auto store_chunk = [&](int buf) {
+  // LDS byte offsets of this thread's A / B writes (fixed across chunks)
+  int a_woff[A_LD], b_woff[B_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int r = (tid >> 3) + (NT / 8) * i;
+    a_woff[i] = r * ROWB + (((kq >> 1) ^ ((r >> 2) & 3)) << 4) + ((kq & 1) << 3);
+  }
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int u = tid + NT * j;
+    const int r = u >> 2;
+    b_woff[j] = r * ROWB + (((u & 3) ^ ((r >> 2) & 3)) << 4);
+  }
+
+  auto store_chunk = [&](int buf, auto SET) {
+    constexpr int S = decltype(SET)::value;
     char* st = lds + buf * STAGE;
     char* sah = st;
     char* sal = st + BM * ROWB;
@@ -167,23 +209,22 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     char* sbl = st + (2 * BM + BN) * ROWB;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
-      const int r = (tid >> 3) + (NT / 8) * i;
-      const float4 v = ra[i];
-      overflow |= fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) >= 65504.f;
-      uint2 h, l;
-      split2(v.x, v.y, h.x, l.x);
-      split2(v.z, v.w, h.y, l.y);
-      const int off = r * ROWB + (((kq >> 1) ^ ((r >> 2) & 3)) << 4) + ((kq & 1) << 3);
-      *reinterpret_cast<uint2*>(sah + off) = h;
-      *reinterpret_cast<uint2*>(sal + off) = l;
+      const float4 v = ra[S][i];
+      const half2_t h01 = __builtin_convertvector((float2_t){v.x, v.y}, half2_t);
+      const half2_t h23 = __builtin_convertvector((float2_t){v.z, v.w}, half2_t);
+      const float2_t f01 = __builtin_convertvector(h01, float2_t);
+      const float2_t f23 = __builtin_convertvector(h23, float2_t);
+      const half2_t l01 = __builtin_convertvector((float2_t){v.x - f01.x, v.y - f01.y}, half2_t);
+      const half2_t l23 = __builtin_convertvector((float2_t){v.z - f23.x, v.w - f23.y}, half2_t);
+      *reinterpret_cast<uint2*>(sah + a_woff[i]) =
+          make_uint2(__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23));
+      *reinterpret_cast<uint2*>(sal + a_woff[i]) =
+          make_uint2(__builtin_bit_cast(uint32_t, l01), __builtin_bit_cast(uint32_t, l23));
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      const int u = tid + NT * j;
-      const int r = u >> 2;
-      const int off = r * ROWB + (((u & 3) ^ ((r >> 2) & 3)) << 4);
-      *reinterpret_cast<uint4*>(sbh + off) = rbh[j];
-      *reinterpret_cast<uint4*>(sbl + off) = rbl[j];
+      *reinterpret_cast<uint4*>(sbh + b_woff[j]) = rbh[S][j];
+      *reinterpret_cast<uint4*>(sbl + b_woff[j]) = rbl[S][j];
     }
   };
 
@@ -199,72 +240,92 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // fragment row byte offsets (row part) and swizzle keys, fixed across chunks
-  int a_row_off[TM], a_key[TM], b_row_off[TN], b_key[TN];
+  // fragment read offsets: step s of a chunk reads 16-B slot (2s + hh) of its row (swizzled)
+  int a_roff[2][TM], b_roff[2][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int r = (wm * TM + i) * 32 + li;
-    a_row_off[i] = r * ROWB;
-    a_key[i] = (r >> 2) & 3;
-  }
+  for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int r = (wn * TN + j) * 32 + li;
-    b_row_off[j] = r * ROWB;
-    b_key[j] = (r >> 2) & 3;
+    for (int i = 0; i < TM; ++i) {
+      const int r = (wm * TM + i) * 32 + li;
+      a_roff[s2][i] = r * ROWB + (((2 * s2 + hh) ^ ((r >> 2) & 3)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r = (wn * TN + j) * 32 + li;
+      b_roff[s2][j] = r * ROWB + (((2 * s2 + hh) ^ ((r >> 2) & 3)) << 4);
+    }
   }
 
   const int nk = (K + BK - 1) / BK;
-  load_chunk(0);
-  store_chunk(0);
-  __syncthreads();
+  const std::integral_constant<int, 0> I0;
+  const std::integral_constant<int, 1> I1;
 
-  for (int kc = 0; kc < nk; ++kc) {
-    const int cur = kc & 1;
-    const bool more = kc + 1 < nk;
-    if (more) load_chunk((kc + 1) * BK);
+  auto compute = [&](int cur) {
     const char* st = lds + cur * STAGE;
     const char* sah = st;
     const char* sal = st + BM * ROWB;
     const char* sbh = st + 2 * BM * ROWB;
     const char* sbl = st + (2 * BM + BN) * ROWB;
+    half8 ah[2][TM], al[2][TM], bh[2][TN], bl[2][TN];
 #pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const int slot = 2 * s + hh;
-      half8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int off = a_row_off[i] + ((slot ^ a_key[i]) << 4);
-        ah[i] = *reinterpret_cast<const half8*>(sah + off);
-        al[i] = *reinterpret_cast<const half8*>(sal + off);
-      }
+    for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int off = b_row_off[j] + ((slot ^ b_key[j]) << 4);
-        bh[j] = *reinterpret_cast<const half8*>(sbh + off);
-        bl[j] = *reinterpret_cast<const half8*>(sbl + off);
+        bh[s2][j] = *reinterpret_cast<const half8*>(sbh + b_roff[s2][j]);
+        bl[s2][j] = *reinterpret_cast<const half8*>(sbl + b_roff[s2][j]);
       }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        ah[s2][i] = *reinterpret_cast<const half8*>(sah + a_roff[s2][i]);
+        al[s2][i] = *reinterpret_cast<const half8*>(sal + a_roff[s2][i]);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
       // small terms first, the hi x hi term last (independent accumulators interleaved)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2][i], bh[s2][j], acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2][i], bl[s2][j], acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2][i], bh[s2][j], acc[i][j], 0, 0, 0);
     }
-    if (more) store_chunk(cur ^ 1);
+  };
+  // iteration kc: MFMAs on LDS buffer kc&1, then chunk kc+1 (register set NEXT) -> LDS buffer
+  // (kc+1)&1 and chunk kc+3's loads into the freed set; chunk kc+2 stays in flight meanwhile.
+  // Every load / store is unconditional (chunks past K read as zeros through the OOB offset, and the
+  // K loop runs to an even count): a conditional load would make hipcc's vmcnt bookkeeping fall
+  // back to vmcnt(0) and drain the chunk kept in flight.
+  auto iteration = [&](int kc, auto NEXT) {
+    compute(kc & 1);
+    store_chunk((kc + 1) & 1, NEXT);
+    load_chunk(NEXT, (kc + 3) * BK);
     __syncthreads();
+  };
+
+  load_chunk(I0, 0);
+  load_chunk(I1, BK);
+  store_chunk(0, I0);
+  load_chunk(I0, 2 * BK);
+  __syncthreads();
+  for (int kc = 0; kc < nk; kc += 2) {
+    iteration(kc, I1);
+    iteration(kc + 1, I0);
   }
 
-  if (overflow && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
-
   // ---- fused epilogue. C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  // An activation beyond the fp16 range (|x| >= 65504) makes its hi part infinite, so every output
+  // it feeds becomes inf / NaN: a non-finite result raises DD_NUM_F16_OVERFLOW.
+  bool bad = false;
   float scl_v[TN], bias_v[TN];
   int ncol[TN];
 #pragma unroll
@@ -274,6 +335,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     bias_v[j] = (a.bias && nv) ? a.bias[ncol[j]] : 0.f;
     scl_v[j] = nv ? a.wsinv[ncol[j]] * a.alpha : 0.f;
   }
+  float* out = a.out;
+  const float* res = a.res;
   const int osh = (int)a.out_sh, osw = (int)a.out_sw;
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
 #pragma unroll
@@ -294,7 +357,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             if (ncol[j] < a.Cout) {
-              float v = acc[i][j][q * 4 + e] * scl_v[j] + bias_v[j];
+              const float acc_v = acc[i][j][q * 4 + e];
+              bad |= !__builtin_isfinite(acc_v);
+              float v = acc_v * scl_v[j] + bias_v[j];
               if (rrow) v += rrow[ncol[j]];
               if (a.relu) v = fmaxf(v, 0.f);
               orow[ncol[j]] = v;
@@ -311,6 +376,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
       }
     }
   }
+  if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
 template <int WM, int WN, int TM, int TN>
@@ -319,7 +385,7 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   const int ntm = (M + BM - 1) / BM;
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
-  if (a.Cin % BK == 0)
+  if (a.Cin % BK == 0 && a.KH * a.KW <= 32)
     hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
   else
     hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 0>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
@@ -347,17 +413,20 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if ((int64_t)a.Ho * a.out_sh >= (int64_t(1) << 31) || (int64_t)a.Ho * a.res_sh >= (int64_t(1) << 31))
     throw std::runtime_error("conv_x3: per-image output extent too large");
   const int64_t t128 = ((M + 127) / 128) * (int64_t)((a.Cout + 127) / 128);
+  const int64_t t256 = ((M + 255) / 256) * (int64_t)((a.Cout + 127) / 128);
+  static const int big = getenv("DDMI_X3_BIG") ? atoi(getenv("DDMI_X3_BIG")) : 0;
+  const bool generic = !(a.Cin % BK == 0 && a.KH * a.KW <= 32);
   if (a.Cout <= 64) {
-    if ((M + 255) / 256 >= 256)
+    if (!generic && (M + 255) / 256 >= 256)
       launch_x3_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64
     else
       launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
+  } else if (big && t256 >= 256) {
+    launch_x3_cfg<2, 2, 4, 2>(a, M, K, st);    // 256 x 128, one 4-wave WG per CU
   } else if (t128 >= 512) {
     launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);    // 128 x 128
-  } else if (t128 * 4 >= 512) {
-    launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);    // 64 x 64
   } else {
-    launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);
+    launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);    // 64 x 64
   }
 }
 

@@ -443,7 +443,7 @@ class Model {
     a.relu = relu;
     use_split(a, c.x3);
     const double fl = 2.0 * N * a.Ho * a.Wo * (double)c.cout * c.k * c.k * c.cin_real;
-    launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
+    launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
   // contiguous NHWC conv; returns output spatial size
   void conv_c(const Conv& c, const float* in, int N, int H, int Wd, float* out, bool relu, const float* res = nullptr) {
@@ -485,7 +485,7 @@ class Model {
     a.relu = relu;
     use_split(a, L.x3);
     const double fl = 2.0 * G * R * (double)L.nout * L.nin;
-    launch("conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
+    launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
 
   void ln(const LNp& p, const float* x, int64_t ldx, float* y, int64_t ldy, int rows, const float* res = nullptr,

@@ -7,7 +7,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps ${PMC_STEPS:-2} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+ARGS="--steps ${PMC_STEPS:-2} --warmup 1 --no-cpu-baseline --no-compare ${BENCH_ARGS:-}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/pmc_trace" -o run -- python "$R/bench.py" $ARGS > "$R/gpurun_out/pmc_trace.log" 2>&1
 rc=$?; echo "[trace] rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -f csv -d "$R/gpurun_out/pmc_fetch" -o run -- python "$R/bench.py" $ARGS > "$R/gpurun_out/pmc_fetch.log" 2>&1

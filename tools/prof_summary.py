@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--forwards", type=int, default=0, help="forward passes in the trace (for per-forward numbers)")
     ap.add_argument("--pmc", nargs="*", default=[])
     ap.add_argument("--note", default="")
+    ap.add_argument("--pmc-kernel", default="conv_gemm", help="kernel class whose HBM bytes per launch to derive")
     a = ap.parse_args()
     rows = load_trace(a.trace_dir)
     if not rows:
@@ -93,14 +94,15 @@ def main():
         for k, ctrs in pmc.items():
             res["pmc"][k] = {c: {"sum": v[0], "dispatches": v[1], "per_launch": v[0] / max(v[1], 1)}
                              for c, v in ctrs.items()}
-        cg = res["pmc"].get("conv_gemm", {})
+        cg = res["pmc"].get(a.pmc_kernel, {})
+        res["pmc_kernel"] = a.pmc_kernel
         if "FETCH_SIZE" in cg and "WRITE_SIZE" in cg:
             # FETCH_SIZE / WRITE_SIZE are in KB; gfx950 FETCH_SIZE counts half of wide streaming reads
             fetch = cg["FETCH_SIZE"]["per_launch"] * 1024 * 2
             write = cg["WRITE_SIZE"]["per_launch"] * 1024
-            res["conv_gemm_hbm_bytes_per_launch"] = fetch + write
-            res["conv_gemm_fetch_bytes_per_launch_x2"] = fetch
-            res["conv_gemm_write_bytes_per_launch"] = write
+            res["hbm_bytes_per_launch"] = fetch + write
+            res["fetch_bytes_per_launch_x2"] = fetch
+            res["write_bytes_per_launch"] = write
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", a.name + ".json"), "w") as f:
         json.dump(res, f, indent=1)
