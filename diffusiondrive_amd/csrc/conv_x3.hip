@@ -56,7 +56,7 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE>
+template <int WM, int WN, int TM, int TN, int MODE, int DBG = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 - a 32-wide K chunk lies inside one filter tap, the
@@ -210,6 +210,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const float4 v = ra[S][i];
+      if constexpr (DBG & 8) continue;
+      if constexpr (DBG & 1) {  // experiment: raw bits, no split arithmetic
+        *reinterpret_cast<uint2*>(sah + a_woff[i]) = make_uint2(__builtin_bit_cast(uint32_t, v.x), __builtin_bit_cast(uint32_t, v.y));
+        *reinterpret_cast<uint2*>(sal + a_woff[i]) = make_uint2(__builtin_bit_cast(uint32_t, v.z), __builtin_bit_cast(uint32_t, v.w));
+        continue;
+      }
       const half2_t h01 = __builtin_convertvector((float2_t){v.x, v.y}, half2_t);
       const half2_t h23 = __builtin_convertvector((float2_t){v.z, v.w}, half2_t);
       const float2_t f01 = __builtin_convertvector(h01, float2_t);
@@ -223,6 +229,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
+      if constexpr (DBG & 2) {
+        asm volatile("" ::"v"(rbh[S][j].x), "v"(rbl[S][j].x));
+        continue;
+      }
       *reinterpret_cast<uint4*>(sbh + b_woff[j]) = rbh[S][j];
       *reinterpret_cast<uint4*>(sbl + b_woff[j]) = rbl[S][j];
     }
@@ -269,6 +279,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     half8 ah[2][TM], al[2][TM], bh[2][TN], bl[2][TN];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
+      if constexpr (DBG & 16) {  // experiment: no fragment reads
+        for (int j = 0; j < TN; ++j) bh[s2][j] = bl[s2][j] = (half8){};
+        for (int i = 0; i < TM; ++i) ah[s2][i] = al[s2][i] = (half8){};
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bh[s2][j] = *reinterpret_cast<const half8*>(sbh + b_roff[s2][j]);
@@ -279,6 +294,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
         ah[s2][i] = *reinterpret_cast<const half8*>(sah + a_roff[s2][i]);
         al[s2][i] = *reinterpret_cast<const half8*>(sal + a_roff[s2][i]);
       }
+    }
+    if constexpr (DBG & 4) {  // experiment: no MFMAs (fragments kept live)
+      for (int s2 = 0; s2 < 2; ++s2) {
+        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(ah[s2][i]), "v"(al[s2][i]));
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bh[s2][j]), "v"(bl[s2][j]));
+      }
+      return;
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -385,6 +407,20 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   const int ntm = (M + BM - 1) / BM;
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
+  static const int dbg = getenv("DDMI_X3_DBG") ? atoi(getenv("DDMI_X3_DBG")) : 0;
+  if constexpr (WM == 2 && WN == 2 && TM == 2 && TN == 2) {
+    if (dbg && a.Cin % BK == 0 && a.KH * a.KW <= 32) {
+#define DD_DBG(D) \
+  case D: hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, 1, D>), grid, dim3(256), 0, st, a, M, K, ntm, ntn); break;
+      switch (dbg) {
+        DD_DBG(1) DD_DBG(2) DD_DBG(3) DD_DBG(4) DD_DBG(8) DD_DBG(10) DD_DBG(16) DD_DBG(11) DD_DBG(20)
+        default: throw std::runtime_error("bad DDMI_X3_DBG");
+      }
+#undef DD_DBG
+      DD_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   if (a.Cin % BK == 0 && a.KH * a.KW <= 32)
     hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
   else
@@ -421,8 +457,10 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
       launch_x3_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64
     else
       launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
-  } else if (big && t256 >= 256) {
+  } else if (big == 1 && t256 >= 256) {
     launch_x3_cfg<2, 2, 4, 2>(a, M, K, st);    // 256 x 128, one 4-wave WG per CU
+  } else if (big == 2 && t256 >= 256) {
+    launch_x3_cfg<4, 2, 2, 2>(a, M, K, st);    // 256 x 128, one 8-wave WG per CU
   } else if (t128 >= 512) {
     launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);    // 128 x 128
   } else {
