@@ -55,11 +55,17 @@ _SIGS = {
                                        ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]),
     "dd_set_graph": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_set_gemm_mode": (ctypes.c_int, [c_void_p, ctypes.c_int]),
+    "dd_set_schedule": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_get_gemm_mode": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "dd_numerics_flags": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint), ctypes.c_int]),
     "dd_tap": (ctypes.c_int, [c_void_p, ctypes.c_char_p, c_void_p, ctypes.c_size_t,
                               ctypes.POINTER(ctypes.c_size_t), c_void_p]),
     "dd_op_last_error": (ctypes.c_char_p, []),
+    "dd_build_camera": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int,
+                                       ctypes.c_int, c_void_p]),
+    "dd_build_lidar": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int,
+                                      ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                      ctypes.c_int, ctypes.c_longlong, c_void_p]),
     "dd_op_conv2d": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p]),

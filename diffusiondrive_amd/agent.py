@@ -75,7 +75,7 @@ else:
             features = {k: v.unsqueeze(0) for k, v in features.items()}
             with torch.no_grad():
                 predictions = self.forward(features)
-                poses = predictions["trajectory"].squeeze(0).numpy()
+                poses = predictions["trajectory"].squeeze(0).cpu().numpy()
             return Trajectory(poses)
 
         def get_target_builders(self):
@@ -131,8 +131,12 @@ class DiffusionDriveAgent(_Base):
 
     def forward(self, features: Dict[str, torch.Tensor], targets: Dict[str, torch.Tensor] = None,
                 noise: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
-        """transfuser_agent.py:120-125 (eval): returns trajectory plus the auxiliary heads."""
-        return self._transfuser_model.forward(features, noise=noise, heads=True)
+        """transfuser_agent.py:120-125 (eval): returns trajectory plus the auxiliary heads, on the
+        CPU as the reference's CPU-feature forward does (navsim's compute_trajectory calls
+        ``.numpy()`` on it, abstract_agent.py:80-86). Numerics-checked: a f16x3 range overflow
+        re-runs the forward in fp32 (model.forward(safe=True))."""
+        out = self._transfuser_model.forward(features, noise=noise, heads=True, safe=True)
+        return {k: v.cpu() for k, v in out.items()}
 
     def forward_trajectory(self, features, noise=None, steps=None) -> Dict[str, torch.Tensor]:
         """Trajectory-only fast path (no BEV-semantic / agent heads)."""

@@ -60,6 +60,7 @@ struct ConvArgs {
   const float* wsinv = nullptr;
   int64_t ldh = 0;
   unsigned* flags = nullptr;
+  int prec = 0;  // 0 = f16x3 (wh / wl fp16 hi / lo), 1 = bf16 (wh = bf16 image, one product)
 };
 constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
@@ -91,6 +92,14 @@ void launch_softmax_rows(float* x, int64_t ld, int rows, int L, float scale, hip
 void launch_broadcast_rows(const float* src, int nsrc, float* dst, int rows, int C, hipStream_t st);
 // y = act(x) elementwise, n elements; act 0 = mish, 1 = relu.
 void launch_activation(const float* x, float* y, int64_t n, int act, hipStream_t st);
+
+// ----------------------------------------------------------------------------------------
+// Feature builder (features.hip): cams = B x 3 (l0, f0, r0) x H x W x 3 uint8 HWC -> out
+// (B, 3, oh, ow) float NCHW; LiDAR planar xyz per scene at 3 * offs[b] -> (B, C, nb, nb) float.
+void launch_camera_feature(const uint8_t* cams, int B, int H, int W, float* out, int oh, int ow, hipStream_t st);
+void launch_lidar_feature(const float* xyz, const int64_t* offs, int B, int C, float* out, int nb, float lo,
+                          float hi, int ppm, float max_h, float split_h, int hist_max, int64_t max_points,
+                          hipStream_t st);
 
 // ----------------------------------------------------------------------------------------
 // Decoder kernels (decoder.hip)

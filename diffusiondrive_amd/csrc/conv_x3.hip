@@ -39,6 +39,8 @@ namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float float2_t __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -56,12 +58,14 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE, int DBG = 0>
+template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0, int DBG = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 - a 32-wide K chunk lies inside one filter tap, the
   //         tap walk is scalar and each A row carries a precomputed base offset + tap-valid mask;
   // MODE 0: generic K (stem 7x7 on 4 padded channels, small Cin): per-lane tap decode.
+  // PREC 0: f16x3 (hi / lo images of both operands, 3 MFMA products);
+  // PREC 1: bf16 (one bf16 image per operand, 1 MFMA product) - the reduced-precision mode.
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
@@ -70,7 +74,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   static_assert(A_LD >= 1 && BM * (BK / 4) % NT == 0, "A tile / threads");
   static_assert(B_LD >= 1 && BN * 4 % NT == 0, "B tile / threads");
   constexpr int ROWB = BK * 2;                       // 64-B LDS rows (32 halfs)
-  constexpr int STAGE = (2 * BM + 2 * BN) * ROWB;   // Ah, Al, Bh, Bl
+  constexpr int NIMG = PREC == 0 ? 2 : 1;             // images per operand
+  constexpr int STAGE = NIMG * (BM + BN) * ROWB;      // Ah, [Al], Bh, [Bl]
   __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
   const int tid = threadIdx.x;
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
       const int kb = k0 + ((tid + NT * j) & 3) * 8;
       const uint32_t off = (bok[j] && kb < Kp) ? boff[j] + (uint32_t)k0 * 2u : kOOB;
       rbh[S][j] = bload16(rwh, off);
-      rbl[S][j] = bload16(rwl, off);
+      if constexpr (PREC == 0) rbl[S][j] = bload16(rwl, off);
     }
   };
 
@@ -205,12 +210,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     char* st = lds + buf * STAGE;
     char* sah = st;
     char* sal = st + BM * ROWB;
-    char* sbh = st + 2 * BM * ROWB;
-    char* sbl = st + (2 * BM + BN) * ROWB;
+    char* sbh = st + NIMG * BM * ROWB;
+    char* sbl = st + (NIMG * BM + BN) * ROWB;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const float4 v = ra[S][i];
       if constexpr (DBG & 8) continue;
+      if constexpr (PREC == 1) {
+        const bf16x2 b01 = __builtin_convertvector((float2_t){v.x, v.y}, bf16x2);
+        const bf16x2 b23 = __builtin_convertvector((float2_t){v.z, v.w}, bf16x2);
+        *reinterpret_cast<uint2*>(sah + a_woff[i]) =
+            make_uint2(__builtin_bit_cast(uint32_t, b01), __builtin_bit_cast(uint32_t, b23));
+        continue;
+      }
       if constexpr (DBG & 1) {  // experiment: raw bits, no split arithmetic
         *reinterpret_cast<uint2*>(sah + a_woff[i]) = make_uint2(__builtin_bit_cast(uint32_t, v.x), __builtin_bit_cast(uint32_t, v.y));
         *reinterpret_cast<uint2*>(sal + a_woff[i]) = make_uint2(__builtin_bit_cast(uint32_t, v.z), __builtin_bit_cast(uint32_t, v.w));
@@ -234,7 +246,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
         continue;
       }
       *reinterpret_cast<uint4*>(sbh + b_woff[j]) = rbh[S][j];
-      *reinterpret_cast<uint4*>(sbl + b_woff[j]) = rbl[S][j];
+      if constexpr (PREC == 0) *reinterpret_cast<uint4*>(sbl + b_woff[j]) = rbl[S][j];
     }
   };
 
@@ -274,9 +286,28 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     const char* st = lds + cur * STAGE;
     const char* sah = st;
     const char* sal = st + BM * ROWB;
-    const char* sbh = st + 2 * BM * ROWB;
-    const char* sbl = st + (2 * BM + BN) * ROWB;
+    const char* sbh = st + NIMG * BM * ROWB;
+    const char* sbl = st + (NIMG * BM + BN) * ROWB;
     half8 ah[2][TM], al[2][TM], bh[2][TN], bl[2][TN];
+    if constexpr (PREC == 1) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bh[s2][j] = *reinterpret_cast<const half8*>(sbh + b_roff[s2][j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) ah[s2][i] = *reinterpret_cast<const half8*>(sah + a_roff[s2][i]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ah[s2][i]),
+                                                               __builtin_bit_cast(bf16x8, bh[s2][j]), acc[i][j], 0,
+                                                               0, 0);
+      return;
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       if constexpr (DBG & 16) {  // experiment: no fragment reads
@@ -409,9 +440,9 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   dim3 grid(ntm * ntn, 1, 1);
   static const int dbg = getenv("DDMI_X3_DBG") ? atoi(getenv("DDMI_X3_DBG")) : 0;
   if constexpr (WM == 2 && WN == 2 && TM == 2 && TN == 2) {
-    if (dbg && a.Cin % BK == 0 && a.KH * a.KW <= 32) {
+    if (dbg && a.prec == 0 && a.Cin % BK == 0 && a.KH * a.KW <= 32) {
 #define DD_DBG(D) \
-  case D: hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, 1, D>), grid, dim3(256), 0, st, a, M, K, ntm, ntn); break;
+  case D: hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, 1, 0, D>), grid, dim3(256), 0, st, a, M, K, ntm, ntn); break;
       switch (dbg) {
         DD_DBG(1) DD_DBG(2) DD_DBG(3) DD_DBG(4) DD_DBG(8) DD_DBG(10) DD_DBG(16) DD_DBG(11) DD_DBG(20)
         default: throw std::runtime_error("bad DDMI_X3_DBG");
@@ -421,10 +452,17 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
       return;
     }
   }
-  if (a.Cin % BK == 0 && a.KH * a.KW <= 32)
+  const bool walk = a.Cin % BK == 0 && a.KH * a.KW <= 32;
+  if (a.prec == 1) {
+    if (walk)
+      hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+    else
+      hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 0, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+  } else if (walk) {
     hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
-  else
+  } else {
     hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 0>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+  }
   DD_HIP_CHECK(hipGetLastError());
 }
 
@@ -432,7 +470,7 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if (a.Cin % 4 != 0) throw std::runtime_error("conv_x3: Cin must be a multiple of 4");
   if ((a.in_sw % 4) || (a.in_sh % 4) || (a.in_sn % 4) || (reinterpret_cast<uintptr_t>(a.in) % 16))
     throw std::runtime_error("conv_x3: input strides / base must be 16-byte aligned");
-  if (!a.wh || !a.wl || !a.wsinv) throw std::runtime_error("conv_x3: missing split weights");
+  if (!a.wh || (a.prec == 0 && !a.wl) || !a.wsinv) throw std::runtime_error("conv_x3: missing split weights");
   if ((a.ldh % 8) || (reinterpret_cast<uintptr_t>(a.wh) % 16) || (reinterpret_cast<uintptr_t>(a.wl) % 16))
     throw std::runtime_error("conv_x3: split weight rows must be 16-byte aligned");
   if (a.batch != 1 || a.b_kn) throw std::runtime_error("conv_x3: batched / KN operands are not supported");

@@ -118,6 +118,24 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
   });
 }
 
+int dd_build_camera(const uint8_t* cams, int B, int src_h, int src_w, float* out, int out_h, int out_w,
+                    void* stream) {
+  return op_guard([&] {
+    if (!cams || !out) throw std::invalid_argument("null pointer");
+    launch_camera_feature(cams, B, src_h, src_w, out, out_h, out_w, S(stream));
+  });
+}
+
+int dd_build_lidar(const float* xyz, const int64_t* offsets, int B, int channels, float* out, int resolution,
+                   float range_lo, float range_hi, int pixels_per_meter, float max_height, float split_height,
+                   int hist_max, long long max_points, void* stream) {
+  return op_guard([&] {
+    if (!offsets || !out || (!xyz && max_points > 0)) throw std::invalid_argument("null pointer");
+    launch_lidar_feature(xyz, offsets, B, channels, out, resolution, range_lo, range_hi, pixels_per_meter,
+                         max_height, split_height, hist_max, max_points, S(stream));
+  });
+}
+
 int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,
                int relu, void* stream) {
   return op_guard([&] {

@@ -111,7 +111,8 @@ class Model {
   std::map<std::string, std::pair<float*, size_t>> bufs;
   bool profiling = false;
   bool use_graph = true;
-  int gemm_mode = DD_GEMM_FP32;       // DD_GEMM_FP32 | DD_GEMM_F16X3 (dd_set_gemm_mode)
+  int gemm_mode = DD_GEMM_FP32;       // DD_GEMM_FP32 | DD_GEMM_F16X3 | DD_GEMM_BF16 (dd_set_gemm_mode)
+  int schedule = DD_SCHED_TRUNCATED;  // DD_SCHED_TRUNCATED (reference) | DD_SCHED_VANILLA (C5 ablation)
   unsigned* num_flags = nullptr;      // device word: DD_NUM_* bits raised by kernels
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;
@@ -139,7 +140,8 @@ class Model {
     if (const char* g = getenv("DDMI_GEMM")) {
       if (!strcmp(g, "fp32")) gemm_mode = DD_GEMM_FP32;
       else if (!strcmp(g, "f16x3")) gemm_mode = DD_GEMM_F16X3;
-      else throw std::invalid_argument(std::string("DDMI_GEMM must be fp32 or f16x3, got ") + g);
+      else if (!strcmp(g, "bf16")) gemm_mode = DD_GEMM_BF16;
+      else throw std::invalid_argument(std::string("DDMI_GEMM must be fp32, f16x3 or bf16, got ") + g);
     }
     DD_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     DD_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
@@ -402,8 +404,9 @@ class Model {
 
   // route a conv / linear to the f16x3 split-MFMA kernel when that mode is on
   void use_split(ConvArgs& a, const SplitW& x) {
-    if (gemm_mode != DD_GEMM_F16X3 || x.hi == kNone) return;
-    a.wh = reinterpret_cast<const uint16_t*>(W(x.hi));
+    if (gemm_mode == DD_GEMM_FP32 || x.hi == kNone) return;
+    a.prec = gemm_mode == DD_GEMM_BF16 ? 1 : 0;
+    a.wh = reinterpret_cast<const uint16_t*>(W(a.prec ? x.b16 : x.hi));
     a.wl = reinterpret_cast<const uint16_t*>(W(x.lo));
     a.wsinv = W(x.sinv);
     a.ldh = x.ldh;
@@ -786,9 +789,12 @@ class Model {
       gemm_g(w.ag_kv, agents, (int64_t)NQ * d, d, B, 30, akv[l], (int64_t)30 * 2 * d, 2 * d);
     }
     float* imgx = buf("ddim_img", (size_t)R * P * 2);
+    const bool vanilla = schedule == DD_SCHED_VANILLA;
     {
+      // truncated: add_noise(norm_odo(anchor), noise, t = trunc_timestep) (:593-597);
+      // vanilla (C5 ablation): x_T = noise (sa = 0, s1a = 1 keep it bit-exact)
       const float a8 = ac[cfg.trunc_timestep];
-      const float sa = std::sqrt(a8), s1a = std::sqrt(1.0f - a8);
+      const float sa = vanilla ? 0.0f : std::sqrt(a8), s1a = vanilla ? 1.0f : std::sqrt(1.0f - a8);
       launch("misc", 0, [&] { launch_ddim_init(W(anchor), noise, imgx, B, Q * P, sa, s1a, st); });
     }
     float* pts = buf("pts", (size_t)R * P * 2);
@@ -811,10 +817,14 @@ class Model {
     float* r1 = buf("dr1", (size_t)R * d);
     float* r2 = buf("dr2", (size_t)R * d);
     float* rr = buf("dr", (size_t)R * P * 3);
-    // roll_timesteps = round(arange(steps) * step_span / steps)[::-1]  (:585-588; numpy round-half-even)
+    // truncated: roll_timesteps = round(arange(steps) * step_span / steps)[::-1] (:585-588; numpy
+    // round-half-even), DDIM prev = t - 1 (set_timesteps(1000), :584);
+    // vanilla: diffusers "leading" set_timesteps(steps): t_i = (steps-1-i) * (1000 / steps), prev = t - ratio.
     std::vector<int> roll(steps);
+    const int ratio = vanilla ? 1000 / steps : 1;
     for (int s = 0; s < steps; ++s)
-      roll[steps - 1 - s] = (int)std::nearbyint((double)s * ((double)cfg.step_span / (double)steps));
+      roll[steps - 1 - s] = vanilla ? s * ratio
+                                    : (int)std::nearbyint((double)s * ((double)cfg.step_span / (double)steps));
     float* reg_last = nullptr;
     float* cls_last = nullptr;
     for (int si = 0; si < steps; ++si) {
@@ -875,7 +885,7 @@ class Model {
       }
       if (si + 1 < steps) {
         const float a_t = ac[k];
-        const float a_p = (k - 1 >= 0) ? ac[k - 1] : 1.0f;
+        const float a_p = (k - ratio >= 0) ? ac[k - ratio] : 1.0f;
         launch("misc", 0, [&] { launch_ddim_step(reg_last, imgx, R, P, a_t, a_p, st); });
       }
     }
@@ -915,7 +925,8 @@ class Model {
   void forward(const float* camera, const float* lidar, const float* status, const float* noise, int B, int steps,
                const Outs& o, hipStream_t caller) {
     if (B <= 0) throw std::invalid_argument("batch must be positive");
-    if (steps <= 0 || steps > cfg.step_span) throw std::invalid_argument("steps must be in [1, step_span]");
+    if (steps <= 0 || steps > (schedule == DD_SCHED_VANILLA ? 1000 : cfg.step_span))
+      throw std::invalid_argument("steps must be in [1, step_span] (truncated) or [1, 1000] (vanilla)");
     if (!camera || !lidar || !status || !noise || !o.traj) throw std::invalid_argument("null input/output pointer");
     DD_HIP_CHECK(hipSetDevice(device));
     // order the handle's stream after the caller's stream, run everything there, then hand back
@@ -926,7 +937,7 @@ class Model {
     stage_inputs(camera, lidar, status, noise, B);
     if (generation != gen0) known_shapes.clear();
     const std::string key = std::to_string(B) + "/" + std::to_string(steps) + "/" + std::to_string(heads) + "/g" +
-                            std::to_string(gemm_mode);
+                            std::to_string(gemm_mode) + "/s" + std::to_string(schedule);
     if (use_graph && !profiling && known_shapes.count(key)) {
       const std::string gkey = key + "#" + std::to_string(generation);
       if (graph.key != gkey) {
@@ -1083,9 +1094,20 @@ int dd_set_graph(dd_handle* h, int enable) {
 int dd_set_gemm_mode(dd_handle* h, int mode) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
-    if (mode != DD_GEMM_FP32 && mode != DD_GEMM_F16X3) throw std::invalid_argument("unknown gemm mode");
+    if (mode != DD_GEMM_FP32 && mode != DD_GEMM_F16X3 && mode != DD_GEMM_BF16)
+      throw std::invalid_argument("unknown gemm mode");
     std::lock_guard<std::mutex> lk(h->mu);
     h->m->gemm_mode = mode;
+  });
+}
+
+int dd_set_schedule(dd_handle* h, int schedule) {
+  return guarded([&] {
+    if (!h) throw std::invalid_argument("null handle");
+    if (schedule != DD_SCHED_TRUNCATED && schedule != DD_SCHED_VANILLA)
+      throw std::invalid_argument("unknown schedule");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->m->schedule = schedule;
   });
 }
 

@@ -111,9 +111,11 @@ SplitW prep_split(Arena& ar, const float* w, int rows, int K) {
   const size_t nh = (size_t)rows * x.ldh;  // halfs per image
   x.hi = ar.add_zero((nh + 1) / 2);
   x.lo = ar.add_zero((nh + 1) / 2);
+  x.b16 = ar.add_zero((nh + 1) / 2);
   std::vector<float> sinv(rows, 1.f);
   _Float16* hi = reinterpret_cast<_Float16*>(ar.host(x.hi));
   _Float16* lo = reinterpret_cast<_Float16*>(ar.host(x.lo));
+  __bf16* b16 = reinterpret_cast<__bf16*>(ar.host(x.b16));
   for (int r = 0; r < rows; ++r) {
     float amax = 0.f;
     for (int k = 0; k < K; ++k) amax = std::max(amax, std::fabs(w[(size_t)r * K + k]));
@@ -130,6 +132,7 @@ SplitW prep_split(Arena& ar, const float* w, int rows, int K) {
       const _Float16 h = (_Float16)v;
       hi[(size_t)r * x.ldh + k] = h;
       lo[(size_t)r * x.ldh + k] = (_Float16)(v - (float)h);
+      b16[(size_t)r * x.ldh + k] = (__bf16)v;
     }
   }
   x.sinv = ar.add(sinv);

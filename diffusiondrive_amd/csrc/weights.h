@@ -49,6 +49,7 @@ class Arena {
 // per-row inverse power-of-two scale (float[rows]).
 struct SplitW {
   size_t hi = kNone, lo = kNone, sinv = kNone;
+  size_t b16 = kNone;  // bf16 image (RNE) of the same scaled weights, for DD_GEMM_BF16
   int ldh = 0;
 };
 // Conv weights re-laid out as [Cout][KH][KW][Cin_pad] (B operand "NK" of conv_gemm), BN folded.

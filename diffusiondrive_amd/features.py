@@ -1,98 +1,118 @@
-"""Input feature builder (the input side of the boundary).
+"""Input feature builder on the GPU (the input side of the boundary).
 
 Mirrors ``TransfuserFeatureBuilder`` (transfuser_features.py:25-138) so ``compute_trajectory``
-works end to end on an ``AgentInput``:
+works end to end on an ``AgentInput``, with the per-pixel / per-point work in HIP kernels
+(``csrc/features.hip`` through the C ABI ``dd_build_camera`` / ``dd_build_lidar``):
 
-* camera: l0 / f0 / r0 crops [28:-28, 416:-416] / [28:-28] stitched side by side, resized to
-  1024x256 with OpenCV ``INTER_LINEAR`` semantics, ``ToTensor`` (HWC uint8 -> CHW float / 255).
-  cv2 is not installed here; for uint8 input and an exact integer down-scale factor f (the NAVSIM
-  case: 4096x1024 -> 1024x256, f = 4) cv2's fixed-point INTER_LINEAR reduces to
-  ``floor((p00 + p01 + p10 + p11 + 2) / 4)`` over the 2x2 source block at ``f*d + f/2 - 1``
-  (coefficients 0.5/0.5 in Q11, final shift 22 with rounding), which is what this computes.
-  Other sizes use a float bilinear resize (parity vs cv2 unpinned there).
-* LiDAR: ``np.histogramdd`` splat of points with z in (0.2, 100) over 256x256 bins of
-  [-32, 32] m, clipped at 5, divided by 5 (transfuser_features.py:79-138).
-* status: [driving_command one-hot (4), ego_velocity (2), ego_acceleration (2)] (:46-53).
+* camera: the raw l0 / f0 / r0 uint8 images go to the device as-is (18.7 MB per scene instead of
+  a CPU stitch + cv2 resize); one kernel crops, stitches, resizes (cv2 INTER_LINEAR at the exact
+  4x NAVSIM factor) and converts to float CHW / 255.
+* LiDAR: ``lidar_pc[:3]`` (contiguous planar x, y, z rows of NAVSIM's (6, N) array) goes to the
+  device unchanged; one atomic histogram pass + an in-place finalize produce the (C, 256, 256)
+  splat (``np.histogramdd`` semantics, bit-exact; tests/golden/lidar_feat_*.npz).
+* status: [driving_command (4), ego_velocity (2), ego_acceleration (2)] (:46-53), 8 floats.
+
+Features are returned as DEVICE tensors (the forward consumes them in place). There is no CPU
+fallback: without libddmi.so or a GPU this raises. The CPU restatement used to check it lives in
+``oracle/features.py`` (test infrastructure).
 """
-from typing import Dict
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
 
+from . import _lib
 from .config import TransfuserConfig
 
 
-def _resize_linear_uint8(img: np.ndarray, out_w: int, out_h: int) -> np.ndarray:
-    h, w = img.shape[:2]
-    if img.dtype == np.uint8 and h % out_h == 0 and w % out_w == 0 and h // out_h == w // out_w \
-            and (h // out_h) % 2 == 0:
-        f = h // out_h
-        o = f // 2 - 1
-        a = img[o::f][:out_h].astype(np.int32)
-        b = img[o + 1::f][:out_h].astype(np.int32)
-        s = a[:, o::f][:, :out_w] + a[:, o + 1::f][:, :out_w] + b[:, o::f][:, :out_w] + b[:, o + 1::f][:, :out_w]
-        return ((s + 2) >> 2).astype(np.uint8)
-    # generic float bilinear, align_corners=False (cv2 INTER_LINEAR geometry)
-    x = img.astype(np.float32)
-    ys = np.clip((np.arange(out_h) + 0.5) * h / out_h - 0.5, 0, h - 1)
-    xs = np.clip((np.arange(out_w) + 0.5) * w / out_w - 0.5, 0, w - 1)
-    y0, x0 = np.floor(ys).astype(int), np.floor(xs).astype(int)
-    y1, x1 = np.minimum(y0 + 1, h - 1), np.minimum(x0 + 1, w - 1)
-    ly, lx = (ys - y0)[:, None, None], (xs - x0)[None, :, None]
-    r = (x[y0][:, x0] * (1 - lx) + x[y0][:, x1] * lx) * (1 - ly) + (x[y1][:, x0] * (1 - lx) + x[y1][:, x1] * lx) * ly
-    return np.clip(np.rint(r), 0, 255).astype(np.uint8) if img.dtype == np.uint8 else r
+def _device(device: Optional[int]) -> torch.device:
+    if not torch.cuda.is_available():
+        raise _lib.DDMIUnavailable("the feature builder runs on the GPU (torch.cuda.is_available() is False)")
+    return torch.device(f"cuda:{torch.cuda.current_device() if device is None else int(device)}")
 
 
-def camera_feature(cam_l0: np.ndarray, cam_f0: np.ndarray, cam_r0: np.ndarray, cfg: TransfuserConfig) -> torch.Tensor:
-    l0 = cam_l0[28:-28, 416:-416]
-    f0 = cam_f0[28:-28]
-    r0 = cam_r0[28:-28, 416:-416]
-    stitched = np.concatenate([l0, f0, r0], axis=1)
-    resized = _resize_linear_uint8(stitched, cfg.camera_width, cfg.camera_height)
-    t = torch.from_numpy(np.ascontiguousarray(resized.transpose(2, 0, 1)))
-    return t.float().div(255.0) if resized.dtype == np.uint8 else t.float()
+def camera_features(images: Sequence[Sequence[np.ndarray]], cfg: TransfuserConfig,
+                    device: Optional[int] = None) -> torch.Tensor:
+    """images: per scene (cam_l0, cam_f0, cam_r0) uint8 HWC arrays -> (B, 3, H, W) float on the GPU."""
+    lib = _lib.load()
+    dev = _device(device)
+    B = len(images)
+    h, w = images[0][1].shape[:2]
+    for sc in images:
+        for im in sc:
+            if im.dtype != np.uint8 or im.shape != (h, w, 3):
+                raise ValueError(f"camera images must be uint8 ({h}, {w}, 3), got {im.dtype} {im.shape}")
+    host = torch.from_numpy(np.stack([np.stack(sc) for sc in images]))  # (B, 3, h, w, 3)
+    cams = host.pin_memory().to(dev, non_blocking=True) if B > 1 else host.to(dev)
+    out = torch.empty((B, 3, cfg.camera_height, cfg.camera_width), device=dev)
+    s = torch.cuda.current_stream(dev)
+    _lib.check(lib.dd_build_camera(cams.data_ptr(), B, h, w, out.data_ptr(), cfg.camera_height, cfg.camera_width,
+                                   s.cuda_stream), lib, op=True)
+    out.record_stream(s)
+    cams.record_stream(s)
+    return out
 
 
-def lidar_feature(points_xyz: np.ndarray, cfg: TransfuserConfig) -> torch.Tensor:
-    """points_xyz: (N, 3) ego-frame points."""
-    pc = points_xyz[points_xyz[..., 2] < cfg.max_height_lidar]
-    above = pc[pc[..., 2] > cfg.lidar_split_height]
+def lidar_features(points: Sequence[np.ndarray], cfg: TransfuserConfig, device: Optional[int] = None) -> torch.Tensor:
+    """points: per scene a (3, N) float32 planar xyz array (NAVSIM ``lidar_pc[:3]``) ->
+    (B, C, 256, 256) float on the GPU."""
+    lib = _lib.load()
+    dev = _device(device)
+    B = len(points)
+    planes = [np.ascontiguousarray(p[:3], dtype=np.float32) for p in points]
+    counts = np.array([p.shape[1] for p in planes], np.int64)
+    offs = np.zeros(B + 1, np.int64)
+    offs[1:] = np.cumsum(counts)
+    xyz = torch.from_numpy(np.concatenate([p.reshape(-1) for p in planes]) if B else np.zeros(0, np.float32))
+    xyz_d = xyz.to(dev)
+    offs_d = torch.from_numpy(offs).to(dev)
+    C = cfg.lidar_in_channels
+    res = cfg.lidar_resolution_height
+    if cfg.lidar_resolution_width != res:
+        raise ValueError("lidar feature: square BEV grid expected")
+    out = torch.empty((B, C, res, res), device=dev)
+    s = torch.cuda.current_stream(dev)
+    _lib.check(lib.dd_build_lidar(xyz_d.data_ptr() if xyz_d.numel() else None, offs_d.data_ptr(), B, C,
+                                  out.data_ptr(), res, float(cfg.lidar_min_x), float(cfg.lidar_max_x),
+                                  int(cfg.pixels_per_meter), float(cfg.max_height_lidar),
+                                  float(cfg.lidar_split_height), int(cfg.hist_max_per_pixel),
+                                  int(counts.max()) if B else 0, s.cuda_stream), lib, op=True)
+    out.record_stream(s)
+    xyz_d.record_stream(s)
+    offs_d.record_stream(s)
+    return out
 
-    def splat(p):
-        nx = int((cfg.lidar_max_x - cfg.lidar_min_x) * int(cfg.pixels_per_meter)) + 1
-        ny = int((cfg.lidar_max_y - cfg.lidar_min_y) * int(cfg.pixels_per_meter)) + 1
-        xb = np.linspace(cfg.lidar_min_x, cfg.lidar_max_x, nx)
-        yb = np.linspace(cfg.lidar_min_y, cfg.lidar_max_y, ny)
-        hist = np.histogramdd(p[:, :2], bins=(xb, yb))[0]
-        hist[hist > cfg.hist_max_per_pixel] = cfg.hist_max_per_pixel
-        return hist / cfg.hist_max_per_pixel
 
-    feats = [splat(above)]
-    if cfg.use_ground_plane:
-        below = pc[pc[..., 2] <= cfg.lidar_split_height]
-        feats = [splat(below), splat(above)]
-    return torch.tensor(np.stack(feats, axis=0).astype(np.float32))
+def status_features(egos: Sequence, device: Optional[int] = None) -> torch.Tensor:
+    """transfuser_features.py:46-53: [driving_command, ego_velocity, ego_acceleration] per scene."""
+    dev = _device(device)
+    rows = [np.concatenate([np.asarray(e.driving_command, np.float32), np.asarray(e.ego_velocity, np.float32),
+                            np.asarray(e.ego_acceleration, np.float32)]) for e in egos]
+    return torch.from_numpy(np.stack(rows)).to(dev)
 
 
 class TransfuserFeatureBuilder:
-    """transfuser_features.py:25-55 (inference features only)."""
+    """transfuser_features.py:25-55 (inference features only), computed on the GPU."""
 
-    def __init__(self, config: TransfuserConfig):
+    def __init__(self, config: TransfuserConfig, device: Optional[int] = None):
         self._config = config
+        self._device = device
 
     def get_unique_name(self) -> str:
         return "transfuser_feature"
 
     def compute_features(self, agent_input) -> Dict[str, torch.Tensor]:
-        cams = agent_input.cameras[-1]
-        ego = agent_input.ego_statuses[-1]
-        lidar_pc = agent_input.lidars[-1].lidar_pc[0:3].T  # LidarIndex.POSITION (x, y, z)
+        """One scene, as the reference: (3,256,1024), (C,256,256), (8,) - device tensors."""
+        f = self.compute_features_batch([agent_input])
+        return {k: v[0] for k, v in f.items()}
+
+    def compute_features_batch(self, agent_inputs: List) -> Dict[str, torch.Tensor]:
+        """Many scenes at once (batched eval): (B,3,256,1024), (B,C,256,256), (B,8)."""
+        cams = [(a.cameras[-1].cam_l0.image, a.cameras[-1].cam_f0.image, a.cameras[-1].cam_r0.image)
+                for a in agent_inputs]
+        pcs = [a.lidars[-1].lidar_pc[0:3] for a in agent_inputs]  # LidarIndex.POSITION (x, y, z)
         return {
-            "camera_feature": camera_feature(cams.cam_l0.image, cams.cam_f0.image, cams.cam_r0.image, self._config),
-            "lidar_feature": lidar_feature(lidar_pc, self._config),
-            "status_feature": torch.concatenate([
-                torch.tensor(ego.driving_command, dtype=torch.float32),
-                torch.tensor(ego.ego_velocity, dtype=torch.float32),
-                torch.tensor(ego.ego_acceleration, dtype=torch.float32),
-            ]),
+            "camera_feature": camera_features(cams, self._config, self._device),
+            "lidar_feature": lidar_features(pcs, self._config, self._device),
+            "status_feature": status_features([a.ego_statuses[-1] for a in agent_inputs], self._device),
         }

@@ -8,6 +8,8 @@
 device memory and the stream. There is no CPU fallback: without the library or a GPU it raises.
 """
 import ctypes
+import os
+import warnings
 from typing import Dict, Mapping, Optional
 
 import numpy as np
@@ -61,8 +63,13 @@ class DiffusionDriveModel:
     """The DiffusionDrive inference forward on one MI355X (one handle per process/device)."""
 
     def __init__(self, config: Optional[TransfuserConfig] = None, state_dict: Optional[Mapping] = None,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, gemm: Optional[str] = None):
+        """``gemm``: conv / linear arithmetic, 'f16x3' (default: fp32-class 3-product fp16 split
+        MFMA), 'fp32' (fp32 MFMA) or 'bf16' (reduced precision); $DDMI_GEMM overrides the default."""
         self.config = config or TransfuserConfig()
+        self._gemm = gemm or os.environ.get("DDMI_GEMM", "f16x3")
+        if self._gemm not in self.GEMM_MODES:
+            raise ValueError(f"gemm mode must be one of {sorted(self.GEMM_MODES)}, got {self._gemm!r}")
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.DDMIUnavailable("DiffusionDriveModel needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -85,6 +92,7 @@ class DiffusionDriveModel:
         del buf
         self.close()
         self._h = h
+        self.set_gemm_mode(self._gemm)
         return self
 
     def close(self):
@@ -111,7 +119,29 @@ class DiffusionDriveModel:
 
     def forward(self, features: Dict[str, torch.Tensor], noise: Optional[torch.Tensor] = None,
                 steps: Optional[int] = None, heads: bool = False, modes: bool = False,
-                stream: Optional[torch.cuda.Stream] = None) -> Dict[str, torch.Tensor]:
+                stream: Optional[torch.cuda.Stream] = None, safe: bool = False) -> Dict[str, torch.Tensor]:
+        """``safe``: synchronise, and if a kernel raised a numerics flag (f16x3 activation beyond
+        the fp16 range) re-run this forward in fp32 and warn; never returns a flagged result."""
+        if not safe:
+            return self._forward(features, noise, steps, heads, modes, stream)
+        if noise is None:
+            B = torch.as_tensor(features["status_feature"]).shape[0]
+            noise = torch.randn((B, self.config.num_modes, self.config.trajectory_sampling.num_poses, 2))
+        self.numerics_flags(clear=True)
+        out = self._forward(features, noise, steps, heads, modes, stream)
+        if self.numerics_flags(clear=True):
+            mode = self.gemm_mode()
+            warnings.warn(f"ddmi: numerics flag raised in gemm mode {mode!r}; re-running the forward in fp32")
+            self.set_gemm_mode("fp32")
+            try:
+                out = self._forward(features, noise, steps, heads, modes, stream)
+            finally:
+                self.set_gemm_mode(mode)
+            if self.numerics_flags(clear=True):
+                raise _lib.DDMIError("numerics flag raised by the fp32 forward as well")
+        return out
+
+    def _forward(self, features, noise, steps, heads, modes, stream) -> Dict[str, torch.Tensor]:
         cfg = self.config
         cam = features["camera_feature"]
         out_device = cam.device if isinstance(cam, torch.Tensor) else torch.device("cpu")
@@ -170,13 +200,23 @@ class DiffusionDriveModel:
                                    torch.cuda.current_stream(self.device).cuda_stream), self.lib)
         return t if shape is None else t[: int(np.prod(shape))].view(*shape)
 
-    GEMM_MODES = {"fp32": 0, "f16x3": 1}
+    GEMM_MODES = {"fp32": 0, "f16x3": 1, "bf16": 2}
 
     def set_gemm_mode(self, mode: str):
-        """'fp32' (fp32-input MFMA) or 'f16x3' (3-product fp16 split MFMA; include/ddmi.h)."""
+        """'fp32' (fp32-input MFMA), 'f16x3' (3-product fp16 split MFMA, fp32-class) or 'bf16'
+        (one bf16 product per MAC: reduced precision); include/ddmi.h."""
         if mode not in self.GEMM_MODES:
             raise ValueError(f"gemm mode must be one of {sorted(self.GEMM_MODES)}, got {mode!r}")
         _lib.check(self.lib.dd_set_gemm_mode(self.handle, self.GEMM_MODES[mode]), self.lib)
+
+    SCHEDULES = {"truncated": 0, "vanilla": 1}
+
+    def set_schedule(self, schedule: str):
+        """'truncated' (the reference's 2-step truncated DDIM) or 'vanilla' (C5 ablation: x_T = noise,
+        set_timesteps(steps) over 1000 train steps)."""
+        if schedule not in self.SCHEDULES:
+            raise ValueError(f"schedule must be one of {sorted(self.SCHEDULES)}, got {schedule!r}")
+        _lib.check(self.lib.dd_set_schedule(self.handle, self.SCHEDULES[schedule]), self.lib)
 
     def gemm_mode(self) -> str:
         m = ctypes.c_int()

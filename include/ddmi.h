@@ -98,11 +98,23 @@ int dd_set_graph(dd_handle* h, int enable);
  *   DD_GEMM_F16X3  3-product fp16 split on f16 MFMA (conv_x3.hip): each fp32 operand becomes
  *                  hi + lo fp16, products ah*bh + ah*bl + al*bh accumulate in fp32 - fp32-class
  *                  accuracy (<= ~3*2^-22 relative per product) at 5.3x the fp32 MFMA rate.
- * Default DD_GEMM_FP32, or $DDMI_GEMM=fp32|f16x3 at dd_create. Attention score GEMMs stay fp32. */
+ *   DD_GEMM_BF16   one bf16 product per MAC (operands rounded to bf16, fp32 accumulation): the
+ *                  REDUCED-precision mode of the bf16 configs (BASELINE configs C2-bf16 / C4),
+ *                  ~0.06-0.08 m waypoint L2 like the reference's bf16 autocast.
+ * Default DD_GEMM_FP32, or $DDMI_GEMM=fp32|f16x3|bf16 at dd_create. Attention score GEMMs stay fp32. */
 #define DD_GEMM_FP32 0
 #define DD_GEMM_F16X3 1
+#define DD_GEMM_BF16 2
 int dd_set_gemm_mode(dd_handle* h, int mode);
 int dd_get_gemm_mode(dd_handle* h, int* mode);
+/* Denoising schedule of the trajectory head:
+ *   DD_SCHED_TRUNCATED  the reference (transfuser_model_v2.py:578-641): anchors noised to t = 8,
+ *                       steps over round(arange(steps) * 20 / steps)[::-1], DDIM prev = t - 1;
+ *   DD_SCHED_VANILLA    ablation C5 (no reference counterpart): x_T = noise, diffusers "leading"
+ *                       set_timesteps(steps) over 1000 train steps, prev = t - 1000 / steps. */
+#define DD_SCHED_TRUNCATED 0
+#define DD_SCHED_VANILLA 1
+int dd_set_schedule(dd_handle* h, int schedule);
 /* Numerics flags raised by kernels since the last clear (synchronises the handle's stream):
  * bit 0 (DD_NUM_F16_OVERFLOW_BIT) = an activation reached |x| >= 65504 under DD_GEMM_F16X3, so that
  * forward's result is not trustworthy (re-run it in DD_GEMM_FP32). clear != 0 resets them. */
@@ -111,6 +123,23 @@ int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear);
 /* Copy a named internal buffer (e.g. "p3", "keyval", "cross_bev", "reg_s0l1") of the last
  * forward into dst (device pointer), at most `count` floats; *actual = buffer length. */
 int dd_tap(dd_handle* h, const char* name, float* dst, size_t count, size_t* actual, void* stream);
+
+/* ---- input feature builder (TransfuserFeatureBuilder.compute_features on the GPU) ---------- */
+/* Camera feature (transfuser_features.py:57-77): crop + stitch + cv2 INTER_LINEAR resize +
+ * ToTensor. cams: device uint8, B scenes x 3 images (cam_l0, cam_f0, cam_r0) x src_h x src_w x 3
+ * (HWC, as NAVSIM loads them); out: device float (B, 3, out_h, out_w). The stitched image must
+ * down-scale by one even integer factor (NAVSIM: 1080x1920 cameras -> 4096x1024 -> 1024x256). */
+int dd_build_camera(const uint8_t* cams, int B, int src_h, int src_w, float* out, int out_h, int out_w,
+                    void* stream);
+/* LiDAR feature (transfuser_features.py:79-138): np.histogramdd splat of the points with
+ * z < max_height (split at split_height; channels = 2 for use_ground_plane: [below, above], 1:
+ * [above]) over resolution^2 bins of [range_lo, range_hi] m, clip at hist_max, / hist_max.
+ * xyz: device float, per scene b the planar rows x, y, z of its N_b points (= NAVSIM
+ * lidar_pc[:3], contiguous) starting at element 3 * offsets[b]; offsets: device int64 [B + 1]
+ * (offsets[0] = 0); max_points = max_b N_b (launch sizing); out: device float (B, channels, res, res). */
+int dd_build_lidar(const float* xyz, const int64_t* offsets, int B, int channels, float* out, int resolution,
+                   float range_lo, float range_hi, int pixels_per_meter, float max_height, float split_height,
+                   int hist_max, long long max_points, void* stream);
 
 /* ---- single-op entry points (parity tests of individual kernels) ---------------------------- */
 /* Last error message of a dd_op_* call on the calling thread. */

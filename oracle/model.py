@@ -264,17 +264,26 @@ def diff_layer(x, pts, bev, agents, ego, temb, sd, p, cfg, value, taps=None, tag
     return reg, cls
 
 
-def trajectory_head(ego_q, agents_q, bev, sd, cfg, noise, steps=None, taps=None):
+def trajectory_head(ego_q, agents_q, bev, sd, cfg, noise, steps=None, taps=None, schedule="truncated"):
     """TrajectoryHead.forward_test (transfuser_model_v2.py:578-641). ``steps`` generalises the
-    hard-coded step_num=2 (:581) for the C5 latency ablation; steps=2 is the reference."""
+    hard-coded step_num=2 (:581) for the C5 latency ablation; steps=2 is the reference.
+    ``schedule="vanilla"`` is the C5 ablation's non-truncated DDIM (no reference counterpart):
+    x_T = noise and diffusers' "leading" set_timesteps(steps) over the 1000 train steps."""
     steps = steps or cfg.denoise_steps
     p = "_trajectory_head"
     B = ego_q.shape[0]
     sched = DDIM(cfg.num_train_timesteps)
-    ratio = cfg.step_span / steps
-    roll = (np.arange(0, steps) * ratio).round()[::-1].copy().astype(np.int64)
-    anchor = sd[p + ".plan_anchor"].unsqueeze(0).repeat(B, 1, 1, 1)
-    img = sched.add_noise(norm_odo(anchor), noise, cfg.trunc_timestep)
+    if schedule == "vanilla":
+        step_ratio = cfg.num_train_timesteps // steps
+        roll = (np.arange(0, steps) * step_ratio)[::-1].copy().astype(np.int64)
+        img = noise.clone()
+        num_inference = steps
+    else:
+        ratio = cfg.step_span / steps
+        roll = (np.arange(0, steps) * ratio).round()[::-1].copy().astype(np.int64)
+        anchor = sd[p + ".plan_anchor"].unsqueeze(0).repeat(B, 1, 1, 1)
+        img = sched.add_noise(norm_odo(anchor), noise, cfg.trunc_timestep)
+        num_inference = cfg.num_train_timesteps
     # value_proj depends only on layer weights + the BEV map: hoisted per layer (exact).
     values = [F.relu(conv(bev, sd, f"{p}.diff_decoder.layers.{l}.cross_bev_attention.value_proj.0", 1, 1, bias=True))
               for l in range(cfg.num_diff_layers)]
@@ -296,7 +305,7 @@ def trajectory_head(ego_q, agents_q, bev, sd, cfg, noise, steps=None, taps=None)
                 taps.put(f"reg_s{si}l{l}", reg)
                 taps.put(f"cls_s{si}l{l}", cls)
             cur = reg[..., :2]
-        img = sched.step(norm_odo(reg[..., :2]), int(k), img, cfg.num_train_timesteps)
+        img = sched.step(norm_odo(reg[..., :2]), int(k), img, num_inference)
     idx = cls.argmax(-1)
     best = reg[torch.arange(B), idx]
     return best, reg, cls
@@ -312,7 +321,7 @@ class OracleModel:
 
     @torch.no_grad()
     def forward(self, camera, lidar, status, noise, steps=None, taps: Optional[Taps] = None,
-                heads=True) -> Dict[str, torch.Tensor]:
+                heads=True, schedule="truncated") -> Dict[str, torch.Tensor]:
         cfg, sd = self.cfg, self.sd
         cam = torch.as_tensor(np.asarray(camera))
         lid = torch.as_tensor(np.asarray(lidar))
@@ -342,7 +351,7 @@ class OracleModel:
             taps.put("cross_bev", cross)
             taps.put("query_out", q)
         ego_q, agents_q = q[:, :1], q[:, 1:]
-        traj, reg, cls = trajectory_head(ego_q, agents_q, cross, sd, cfg, nz, steps, taps)
+        traj, reg, cls = trajectory_head(ego_q, agents_q, cross, sd, cfg, nz, steps, taps, schedule)
         out = {"trajectory": traj, "poses_reg": reg, "poses_cls": cls}
         if heads:
             h = F.relu(conv(p3, sd, "_bev_semantic_head.0", 1, 1, bias=True))

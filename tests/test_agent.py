@@ -1,4 +1,6 @@
-"""Agent surface (drop-in boundary): feature builder on CPU, compute_trajectory on the GPU."""
+"""Agent surface (drop-in boundary): GPU feature builder + compute_trajectory vs the CPU oracle."""
+import glob
+import os
 from dataclasses import dataclass
 from typing import List
 
@@ -7,6 +9,8 @@ import pytest
 import torch
 
 from diffusiondrive_amd.config import TransfuserConfig
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 @dataclass
@@ -51,39 +55,96 @@ def make_agent_input(seed=0, n_points=20000):
     return _AgentInput([ego], [cams], [_Lidar(pts)])
 
 
-def test_feature_builder_shapes_and_lidar_histogram():
-    from diffusiondrive_amd.features import TransfuserFeatureBuilder
-    cfg = TransfuserConfig()
-    ai = make_agent_input()
-    f = TransfuserFeatureBuilder(cfg).compute_features(ai)
-    assert f["camera_feature"].shape == (3, 256, 1024) and f["camera_feature"].dtype == torch.float32
-    assert f["lidar_feature"].shape == (1, 256, 256)
-    assert torch.equal(f["status_feature"], torch.tensor([0, 1, 0, 0, 4.0, 0.3, 0.1, -0.2]))
-    # LiDAR: independent restatement of the splat (transfuser_features.py:111-138)
-    p = ai.lidars[-1].lidar_pc[:3].T
-    p = p[(p[:, 2] < 100) & (p[:, 2] > 0.2)]
-    inside = (p[:, 0] >= -32) & (p[:, 0] <= 32) & (p[:, 1] >= -32) & (p[:, 1] <= 32)
-    ix = np.clip(np.floor((p[inside, 0] + 32) * 4).astype(int), 0, 255)
-    iy = np.clip(np.floor((p[inside, 1] + 32) * 4).astype(int), 0, 255)
-    h = np.zeros((256, 256))
-    np.add.at(h, (ix, iy), 1)
-    assert np.allclose(f["lidar_feature"][0].numpy(), np.minimum(h, 5) / 5)
-    assert 0.0 <= float(f["camera_feature"].min()) and float(f["camera_feature"].max()) <= 1.0
+def test_oracle_lidar_feature_matches_reference_goldens():
+    """The CPU restatement of the LiDAR splat equals the reference builder's own output bit for bit
+    (tests/golden/lidar_feat_*.npz, produced by TransfuserFeatureBuilder._get_lidar_feature)."""
+    from oracle.features import lidar_feature
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "lidar_feat_*.npz"))):
+        with np.load(path, allow_pickle=False) as z:
+            out = lidar_feature(z["points_xyz"], ground_plane=bool(z["ground_plane"]))
+            assert out.dtype == np.float32 and np.array_equal(out, z["feature"]), path
 
 
-def test_camera_resize_4x_matches_generic_bilinear():
-    from diffusiondrive_amd.features import _resize_linear_uint8
+def test_oracle_camera_resize_is_rounded_2x2_mean():
+    from oracle.features import resize_linear_u8
     r = np.random.default_rng(1)
     img = r.integers(0, 256, (64, 256, 3), dtype=np.uint8)
-    fast = _resize_linear_uint8(img, 64, 16).astype(int)
+    fast = resize_linear_u8(img, 64, 16).astype(int)
     ref = ((img[1::4, 1::4].astype(float) + img[1::4, 2::4] + img[2::4, 1::4] + img[2::4, 2::4]) / 4)
     assert np.abs(fast - ref).max() <= 0.5 + 1e-9  # round-half-up of the 2x2 mean
+    const = np.full((1080, 1920, 3), 77, np.uint8)
+    from oracle.features import camera_feature
+    cf = camera_feature(const, const, const)
+    assert cf.shape == (3, 256, 1024) and np.all(cf == np.float32(77) / np.float32(255))
+
+
+def test_feature_builder_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from diffusiondrive_amd import _lib
+    from diffusiondrive_amd.features import TransfuserFeatureBuilder
+    with pytest.raises(_lib.DDMIUnavailable):
+        TransfuserFeatureBuilder(TransfuserConfig()).compute_features(make_agent_input())
+
+
+def _oracle_features(ai, cfg=None):
+    from oracle.features import camera_feature, lidar_feature, status_feature
+    cfg = cfg or TransfuserConfig()
+    c = ai.cameras[-1]
+    e = ai.ego_statuses[-1]
+    return {"camera_feature": torch.from_numpy(camera_feature(c.cam_l0.image, c.cam_f0.image, c.cam_r0.image)),
+            "lidar_feature": torch.from_numpy(lidar_feature(ai.lidars[-1].lidar_pc[:3].T,
+                                                            ground_plane=cfg.use_ground_plane)),
+            "status_feature": torch.from_numpy(status_feature(e.driving_command, e.ego_velocity,
+                                                              e.ego_acceleration))}
+
+
+@pytest.mark.gpu
+def test_gpu_lidar_feature_matches_reference_goldens(gpu):
+    """dd_build_lidar vs the reference builder's outputs: bit-exact, both golden clouds in ONE
+    batched call per channel setting, plus an empty cloud in the middle of the batch."""
+    from diffusiondrive_amd.features import lidar_features
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "lidar_feat_*.npz"))):
+        with np.load(path, allow_pickle=False) as z:
+            pts, ref, ground = z["points_xyz"], z["feature"], bool(z["ground_plane"])
+        cfg = TransfuserConfig(use_ground_plane=ground)
+        batch = [pts.T, np.zeros((3, 0), np.float32), pts[: len(pts) // 3].T]
+        out = lidar_features(batch, cfg, device=0).cpu().numpy()
+        assert np.array_equal(out[0], ref), path
+        assert not out[1].any()
+        from oracle.features import lidar_feature
+        assert np.array_equal(out[2], lidar_feature(pts[: len(pts) // 3], ground_plane=ground))
+
+
+@pytest.mark.gpu
+def test_gpu_camera_feature_matches_oracle(gpu):
+    from diffusiondrive_amd.features import camera_features
+    from oracle.features import camera_feature
+    cfg = TransfuserConfig()
+    r = np.random.default_rng(5)
+    scenes = [tuple(r.integers(0, 256, (1080, 1920, 3), dtype=np.uint8) for _ in range(3)) for _ in range(2)]
+    out = camera_features(scenes, cfg, device=0).cpu().numpy()
+    for b, sc in enumerate(scenes):
+        assert np.array_equal(out[b], camera_feature(*sc)), b
+    with pytest.raises(Exception):
+        camera_features([tuple(im[:, :1000] for im in scenes[0])], cfg, device=0)
+
+
+@pytest.mark.gpu
+def test_gpu_feature_builder_matches_oracle_features(gpu):
+    from diffusiondrive_amd.features import TransfuserFeatureBuilder
+    ai = make_agent_input(9)
+    f = TransfuserFeatureBuilder(TransfuserConfig(), device=0).compute_features(ai)
+    ref = _oracle_features(ai)
+    assert f["camera_feature"].is_cuda
+    for k in ref:
+        assert torch.equal(f[k].cpu(), ref[k]), k
+    assert torch.equal(f["status_feature"].cpu(), torch.tensor([0, 1, 0, 0, 4.0, 0.3, 0.1, -0.2]))
 
 
 @pytest.mark.gpu
 def test_compute_trajectory_matches_oracle(gpu, seeded_sd, tmp_path):
     from diffusiondrive_amd.agent import DiffusionDriveAgent
-    from diffusiondrive_amd.features import TransfuserFeatureBuilder
     from oracle.model import OracleModel
     ckpt = tmp_path / "dd.pth"
     torch.save({"state_dict": {"agent._transfuser_model." + k: torch.from_numpy(np.asarray(v))
@@ -93,7 +154,7 @@ def test_compute_trajectory_matches_oracle(gpu, seeded_sd, tmp_path):
     torch.manual_seed(77)
     traj = agent.compute_trajectory(ai)
     assert traj.poses.shape == (8, 3) and traj.poses.dtype == np.float32
-    f = TransfuserFeatureBuilder(TransfuserConfig()).compute_features(ai)
+    f = _oracle_features(ai)
     torch.manual_seed(77)
     noise = torch.randn(1, 20, 8, 2)
     ref = OracleModel(seeded_sd).forward(f["camera_feature"][None], f["lidar_feature"][None],

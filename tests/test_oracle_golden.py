@@ -68,3 +68,21 @@ def test_oracle_steps_generalise(oracle):
                        heads=False)
     assert np.array_equal(a["trajectory"].numpy(), b["trajectory"].numpy())
     assert c["trajectory"].shape == (1, 8, 3) and np.isfinite(c["trajectory"].numpy()).all()
+
+
+def test_oracle_vanilla_schedule_ignores_anchors(seeded_sd):
+    """C5 vanilla DDIM starts from pure noise: the anchors must not influence the result, while the
+    truncated (reference) schedule depends on them."""
+    import torch
+    from diffusiondrive_amd.weights import synthetic_inputs
+    from oracle.model import OracleModel
+    inp = synthetic_inputs(1, 5)
+    sd2 = dict(seeded_sd)
+    sd2["_trajectory_head.plan_anchor"] = seeded_sd["_trajectory_head.plan_anchor"] * 0.5
+    args = (inp["camera_feature"], inp["lidar_feature"], inp["status_feature"], inp["noise"])
+    a = OracleModel(seeded_sd).forward(*args, steps=3, heads=False, schedule="vanilla")["trajectory"]
+    b = OracleModel(sd2).forward(*args, steps=3, heads=False, schedule="vanilla")["trajectory"]
+    assert torch.equal(a, b)
+    c = OracleModel(sd2).forward(*args, steps=2, heads=False)["trajectory"]
+    d = OracleModel(seeded_sd).forward(*args, steps=2, heads=False)["trajectory"]
+    assert not torch.equal(c, d)

@@ -117,3 +117,68 @@ def test_forward_matches_oracle_batch8(gpu_model, seeded_sd, mode):
              f"modes max err {float((out['poses_reg'] - ref['poses_reg']).abs().max()):.3e}"])
     assert gpu_model.numerics_flags() == 0
     assert l2 <= WAYPOINT_L2_TOL
+
+
+@pytest.mark.parametrize("mode", GEMM_MODES)
+def test_resnet50_config_matches_oracle(mode):
+    """BASELINE config C4: ResNet-50 image trunk (TransfuserConfig.image_architecture="resnet50",
+    LiDAR stays ResNet-34, channels adapt via transfuser_backbone.py:67-93) vs the CPU oracle.
+    Parity here is pinned through the oracle (its ResNet-34 path is golden-pinned; the ResNet-50
+    Bottleneck restatement shares every primitive)."""
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
+    from oracle.model import OracleModel
+    cfg = TransfuserConfig(image_architecture="resnet50")
+    sd = seeded_state_dict(cfg, 3)
+    inp = synthetic_inputs(2, 77, cfg)
+    ref = OracleModel(sd, cfg).forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"],
+                                       inp["noise"], heads=False)
+    m = DiffusionDriveModel(cfg, sd, device=0)
+    m.set_gemm_mode(mode)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    out = m.forward(feats, noise=torch.from_numpy(inp["noise"]))
+    l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
+    _report([f"== resnet50 B=2 gemm={mode}: waypoint L2 vs oracle {l2:.3e}"])
+    assert m.numerics_flags() == 0
+    assert l2 <= WAYPOINT_L2_TOL
+
+
+@pytest.mark.parametrize("mode", GEMM_MODES)
+def test_vanilla_ddim_schedule_matches_oracle(gpu_model, seeded_sd, mode):
+    """C5 ablation: 10-step vanilla (non-truncated) DDIM on the same decoder vs the oracle's
+    restatement of diffusers' leading set_timesteps(10) (no reference counterpart)."""
+    from oracle.model import OracleModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    gpu_model.set_gemm_mode(mode)
+    inp = synthetic_inputs(2, 555)
+    ref = OracleModel(seeded_sd).forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"],
+                                         inp["noise"], steps=10, heads=False, schedule="vanilla")
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    gpu_model.set_schedule("vanilla")
+    try:
+        out = gpu_model.forward(feats, noise=torch.from_numpy(inp["noise"]), steps=10)
+    finally:
+        gpu_model.set_schedule("truncated")
+    l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
+    _report([f"== vanilla DDIM 10 steps B=2 gemm={mode}: waypoint L2 vs oracle {l2:.3e}"])
+    assert l2 <= WAYPOINT_L2_TOL
+
+
+def test_bf16_mode_is_reduced_precision_but_sane(gpu_model, seeded_sd):
+    """DD_GEMM_BF16 (configs C2-bf16 / C4): one bf16 product per MAC. Reported, loosely bounded:
+    the reference's own bf16 autocast is 0.06-0.08 m off fp32."""
+    from oracle.model import OracleModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    inp = synthetic_inputs(4, 1234)
+    ref = OracleModel(seeded_sd).forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"],
+                                         inp["noise"], heads=False)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    gpu_model.set_gemm_mode("bf16")
+    try:
+        out = gpu_model.forward(feats, noise=torch.from_numpy(inp["noise"]))
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
+    _report([f"== bf16 mode B=4: waypoint L2 vs fp32 oracle {l2:.3e} (reduced precision, not parity)"])
+    assert np.isfinite(l2) and l2 < 1.0

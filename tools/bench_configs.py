@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Secondary BASELINE.json configs on one MI355X (the headline config C2 is bench.py's line).
+
+    python tools/bench_configs.py [--out profiles/rNN_configs] [--steps 10]
+
+* C1  batch 1 latency (the reference's per-token NAVSIM eval shape), every gemm mode.
+* C2  batch 64, ResNet-34, 2 truncated DDIM steps: fp32 / f16x3 / bf16 gemm modes.
+* C4  batch 64, ResNet-50 image trunk (nuScenes-style config; LiDAR stays ResNet-34): bf16 (the
+      config's dtype) and the fp32-class modes, with the bf16 waypoint deviation from f16x3.
+* C5  latency curve: truncated DDIM (reference schedule) N = 1..20 steps and vanilla
+      (non-truncated, x_T = noise over 1000 train steps) N = 2..20, batch 64, f16x3.
+All inputs synthetic and seeded, weights seeded random (no checkpoint download), inputs resident
+in HBM, hipGraph replay, device-synchronised wall clock over `steps` forwards after warmup.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def timed(model, feats, noise, steps_ddim, reps, warm=2):
+    for _ in range(warm):
+        out = model.forward(feats, noise=noise, steps=steps_ddim)["trajectory"]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = model.forward(feats, noise=noise, steps=steps_ddim)["trajectory"]
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3, out.detach().cpu().numpy()
+
+
+def l2(a, b):
+    d = (a[..., :2].astype(np.float64) - b[..., :2].astype(np.float64)).reshape(a.shape[0], -1)
+    return float(np.sqrt((d ** 2).sum(-1)).max())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "configs"))
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
+
+    res = {"device": torch.cuda.get_device_name(0), "reps": a.steps, "configs": {}}
+    dev = torch.device("cuda:0")
+
+    def setup(arch, B, seed=1234):
+        cfg = TransfuserConfig(image_architecture=arch)
+        m = DiffusionDriveModel(cfg, seeded_state_dict(cfg, 0), device=0)
+        inp = synthetic_inputs(B, seed, cfg)
+        feats = {k: torch.from_numpy(inp[k]).to(dev) for k in ("camera_feature", "lidar_feature", "status_feature")}
+        return m, feats, torch.from_numpy(inp["noise"]).to(dev)
+
+    # ---- C1 / C2 (ResNet-34)
+    for B, key in ((1, "C1_batch1_latency"), (64, "C2_batch64")):
+        m, feats, noise = setup("resnet34", B)
+        rows, outs = {}, {}
+        for mode in ("fp32", "f16x3", "bf16"):
+            m.set_gemm_mode(mode)
+            ms, outs[mode] = timed(m, feats, noise, 2, a.steps if B > 1 else 5 * a.steps)
+            rows[mode] = {"ms_per_batch": round(ms, 3), "scenes_per_s": round(B / ms * 1e3, 2),
+                          "numerics_flags": m.numerics_flags()}
+        rows["bf16"]["waypoint_l2_vs_f16x3"] = l2(outs["bf16"], outs["f16x3"])
+        rows["fp32"]["waypoint_l2_vs_f16x3"] = l2(outs["fp32"], outs["f16x3"])
+        res["configs"][key] = {"arch": "resnet34", "batch": B, "ddim_steps": 2, "modes": rows}
+        print(key, json.dumps(rows), flush=True)
+        m.close()
+
+    # ---- C4 (ResNet-50 image trunk)
+    m, feats, noise = setup("resnet50", 64)
+    rows, outs = {}, {}
+    for mode in ("bf16", "f16x3", "fp32"):
+        m.set_gemm_mode(mode)
+        ms, outs[mode] = timed(m, feats, noise, 2, a.steps)
+        rows[mode] = {"ms_per_batch": round(ms, 3), "scenes_per_s": round(64 / ms * 1e3, 2),
+                      "numerics_flags": m.numerics_flags()}
+    rows["bf16"]["waypoint_l2_vs_f16x3"] = l2(outs["bf16"], outs["f16x3"])
+    rows["fp32"]["waypoint_l2_vs_f16x3"] = l2(outs["fp32"], outs["f16x3"])
+    res["configs"]["C4_resnet50_batch64"] = {"arch": "resnet50", "batch": 64, "ddim_steps": 2, "modes": rows,
+                                             "gflop_per_scene_note": "SURVEY §8d probe: 162.2 GFLOP/scene"}
+    print("C4", json.dumps(rows), flush=True)
+    m.close()
+
+    # ---- C5 latency curve (f16x3)
+    m, feats, noise = setup("resnet34", 64)
+    m.set_gemm_mode("f16x3")
+    curve = {"truncated": {}, "vanilla": {}}
+    for n in (1, 2, 4, 6, 8, 10, 20):
+        ms, _ = timed(m, feats, noise, n, a.steps)
+        curve["truncated"][n] = round(ms, 3)
+    m.set_schedule("vanilla")
+    for n in (2, 5, 10, 20):
+        ms, _ = timed(m, feats, noise, n, a.steps)
+        curve["vanilla"][n] = round(ms, 3)
+    m.set_schedule("truncated")
+    res["configs"]["C5_ddim_latency_batch64"] = {"arch": "resnet34", "batch": 64, "gemm": "f16x3",
+                                                 "ms_per_batch_by_steps": curve}
+    print("C5", json.dumps(curve), flush=True)
+    m.close()
+
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out + ".json", "w") as f:
+        json.dump(res, f, indent=1)
+    lines = [f"# Secondary configs ({res['device']}, synthetic seeded inputs/weights, hipGraph replay, "
+             f"{a.steps} reps)", "", "| config | gemm | ms / batch | scenes/s | waypoint L2 vs f16x3 |",
+             "|---|---|---|---|---|"]
+    for key, c in res["configs"].items():
+        if "modes" not in c:
+            continue
+        for mode, r in c["modes"].items():
+            lines.append(f"| {key} | {mode} | {r['ms_per_batch']} | {r['scenes_per_s']} | "
+                         f"{r.get('waypoint_l2_vs_f16x3', '-')} |")
+    lines += ["", "C5 latency (ms per batch of 64, f16x3) by DDIM steps:", "",
+              "| schedule | " + " | ".join(f"N={n}" for n in (1, 2, 4, 5, 6, 8, 10, 20)) + " |",
+              "|---|" + "---|" * 8]
+    for sch, cv in curve.items():
+        lines.append(f"| {sch} | " + " | ".join(str(cv.get(n, "-")) for n in (1, 2, 4, 5, 6, 8, 10, 20)) + " |")
+    with open(a.out + ".md", "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
