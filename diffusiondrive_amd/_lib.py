@@ -71,7 +71,7 @@ _SIGS = {
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p]),
     "dd_op_conv2d_x3": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
                                        c_void_p, c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p]),
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p]),
     "dd_op_gemm": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   ctypes.c_int, ctypes.c_int, c_void_p]),
     "dd_op_gemm_batched": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,

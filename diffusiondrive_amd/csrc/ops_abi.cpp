@@ -69,7 +69,7 @@ int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt
 }
 
 int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
-                    const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
+                    const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, int prec,
                     unsigned* flags, void* stream) {
   return op_guard([&] {
     // split the (device) fp32 weights on the host exactly as dd_create does (weights.cpp:prep_split)
@@ -108,7 +108,9 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
     a.stride = stride;
     a.pad = pad;
     a.relu = relu;
-    a.wh = reinterpret_cast<const uint16_t*>(ar.ptr(x.hi));
+    if (prec != 0 && prec != 1) throw std::invalid_argument("prec must be 0 (f16x3) or 1 (bf16)");
+    a.prec = prec;
+    a.wh = reinterpret_cast<const uint16_t*>(ar.ptr(prec ? x.b16 : x.hi));
     a.wl = reinterpret_cast<const uint16_t*>(ar.ptr(x.lo));
     a.wsinv = ar.ptr(x.sinv);
     a.ldh = x.ldh;

@@ -147,10 +147,11 @@ const char* dd_op_last_error(void);
 /* NHWC conv: in (B,H,W,Cin), wgt (Cout,KH,KW,Cin), optional bias (Cout), res (B,Ho,Wo,Cout). */
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
                  const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream);
-/* Same conv on the f16x3 split kernel (weights split on the host as dd_create does; synchronous).
- * flags (device unsigned, nullable) receives DD_NUM_F16_OVERFLOW_BIT. */
+/* Same conv on the split-precision kernel (conv_x3.hip; weights prepared on the host as dd_create
+ * does; synchronous): prec 0 = f16x3, 1 = bf16. flags (device unsigned, nullable) receives
+ * DD_NUM_F16_OVERFLOW_BIT. */
 int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
-                    const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
+                    const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, int prec,
                     unsigned* flags, void* stream);
 /* C (M,N) = A (M,K) . W(N,K)^T [+ bias] [+ res (M,N)] [relu] */
 int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,

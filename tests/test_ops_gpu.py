@@ -97,10 +97,15 @@ def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     xin, win, bin_ = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b)
     rin = g(r.permute(0, 2, 3, 1)) if res else None
     ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(),
-                           rin.data_ptr() if res else None, out.data_ptr(), Cout, k, k, s, p, int(relu),
+                           rin.data_ptr() if res else None, out.data_ptr(), Cout, k, k, s, p, int(relu), 0,
                            flags.data_ptr(), None), gpu)
     close(out.permute(0, 3, 1, 2), ref, 3e-5)
     assert int(flags.item()) == 0
+    # bf16 (reduced precision, one product): same kernel family, bf16-rounding tolerance
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(),
+                           rin.data_ptr() if res else None, out.data_ptr(), Cout, k, k, s, p, int(relu), 1,
+                           flags.data_ptr(), None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 3e-2)
 
 
 def test_conv2d_f16x3_flags_overflow(gpu):
@@ -112,7 +117,7 @@ def test_conv2d_f16x3_flags_overflow(gpu):
     flags = torch.zeros(1, dtype=torch.int32, device=DEV)
     xin, win = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1))
     ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), 1, 8, 8, 32, win.data_ptr(), None, None, out.data_ptr(), 32, 1, 1, 1, 0,
-                           0, flags.data_ptr(), None), gpu)
+                           0, 0, flags.data_ptr(), None), gpu)
     assert int(flags.item()) & 1
 
 

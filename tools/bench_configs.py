@@ -27,18 +27,32 @@ import torch  # noqa: E402
 
 def timed(model, feats, noise, steps_ddim, reps, warm=2):
     for _ in range(warm):
-        out = model.forward(feats, noise=noise, steps=steps_ddim)["trajectory"]
+        model.forward(feats, noise=noise, steps=steps_ddim)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        out = model.forward(feats, noise=noise, steps=steps_ddim)["trajectory"]
+        model.forward(feats, noise=noise, steps=steps_ddim)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps * 1e3, out.detach().cpu().numpy()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    out = model.forward(feats, noise=noise, steps=steps_ddim, modes=True)
+    return ms, {k: v.detach().cpu().numpy() for k, v in out.items()}
 
 
 def l2(a, b):
     d = (a[..., :2].astype(np.float64) - b[..., :2].astype(np.float64)).reshape(a.shape[0], -1)
     return float(np.sqrt((d ** 2).sum(-1)).max())
+
+
+def deviation(o, ref):
+    """Deviation of one gemm mode's outputs from f16x3's on the same batch: waypoint L2 of the
+    selected trajectory (max over scenes), the fraction of scenes selecting the same mode (argmax
+    over the 20 cls logits), and the max per-mode waypoint L2 over all 20 modes (no argmax jump)."""
+    same = o["poses_cls"].argmax(-1) == ref["poses_cls"].argmax(-1)
+    B, Q = o["poses_reg"].shape[:2]
+    return {"waypoint_l2_vs_f16x3": l2(o["trajectory"], ref["trajectory"]),
+            "mode_agreement_vs_f16x3": float(same.mean()),
+            "allmodes_waypoint_l2_vs_f16x3": l2(o["poses_reg"].reshape(B * Q, -1, 3),
+                                               ref["poses_reg"].reshape(B * Q, -1, 3))}
 
 
 def main():
@@ -69,8 +83,8 @@ def main():
             ms, outs[mode] = timed(m, feats, noise, 2, a.steps if B > 1 else 5 * a.steps)
             rows[mode] = {"ms_per_batch": round(ms, 3), "scenes_per_s": round(B / ms * 1e3, 2),
                           "numerics_flags": m.numerics_flags()}
-        rows["bf16"]["waypoint_l2_vs_f16x3"] = l2(outs["bf16"], outs["f16x3"])
-        rows["fp32"]["waypoint_l2_vs_f16x3"] = l2(outs["fp32"], outs["f16x3"])
+        rows["bf16"].update(deviation(outs["bf16"], outs["f16x3"]))
+        rows["fp32"].update(deviation(outs["fp32"], outs["f16x3"]))
         res["configs"][key] = {"arch": "resnet34", "batch": B, "ddim_steps": 2, "modes": rows}
         print(key, json.dumps(rows), flush=True)
         m.close()
@@ -83,8 +97,8 @@ def main():
         ms, outs[mode] = timed(m, feats, noise, 2, a.steps)
         rows[mode] = {"ms_per_batch": round(ms, 3), "scenes_per_s": round(64 / ms * 1e3, 2),
                       "numerics_flags": m.numerics_flags()}
-    rows["bf16"]["waypoint_l2_vs_f16x3"] = l2(outs["bf16"], outs["f16x3"])
-    rows["fp32"]["waypoint_l2_vs_f16x3"] = l2(outs["fp32"], outs["f16x3"])
+    rows["bf16"].update(deviation(outs["bf16"], outs["f16x3"]))
+    rows["fp32"].update(deviation(outs["fp32"], outs["f16x3"]))
     res["configs"]["C4_resnet50_batch64"] = {"arch": "resnet50", "batch": 64, "ddim_steps": 2, "modes": rows,
                                              "gflop_per_scene_note": "SURVEY §8d probe: 162.2 GFLOP/scene"}
     print("C4", json.dumps(rows), flush=True)
@@ -111,14 +125,17 @@ def main():
     with open(a.out + ".json", "w") as f:
         json.dump(res, f, indent=1)
     lines = [f"# Secondary configs ({res['device']}, synthetic seeded inputs/weights, hipGraph replay, "
-             f"{a.steps} reps)", "", "| config | gemm | ms / batch | scenes/s | waypoint L2 vs f16x3 |",
-             "|---|---|---|---|---|"]
+             f"{a.steps} reps)", "",
+             "| config | gemm | ms / batch | scenes/s | waypoint L2 vs f16x3 | mode agreement | all-mode L2 |",
+             "|---|---|---|---|---|---|---|"]
     for key, c in res["configs"].items():
         if "modes" not in c:
             continue
         for mode, r in c["modes"].items():
+            g = lambda k: (f"{r[k]:.3g}" if k in r else "-")  # noqa: E731
             lines.append(f"| {key} | {mode} | {r['ms_per_batch']} | {r['scenes_per_s']} | "
-                         f"{r.get('waypoint_l2_vs_f16x3', '-')} |")
+                         f"{g('waypoint_l2_vs_f16x3')} | {g('mode_agreement_vs_f16x3')} | "
+                         f"{g('allmodes_waypoint_l2_vs_f16x3')} |")
     lines += ["", "C5 latency (ms per batch of 64, f16x3) by DDIM steps:", "",
               "| schedule | " + " | ".join(f"N={n}" for n in (1, 2, 4, 5, 6, 8, 10, 20)) + " |",
               "|---|" + "---|" * 8]
