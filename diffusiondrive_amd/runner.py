@@ -1,0 +1,84 @@
+"""Batched NAVSIM evaluation producer.
+
+The reference evaluates one token at a time: ``agent.compute_trajectory(agent_input)`` per token
+inside ``run_pdm_score.py:72-102`` / ``run_create_submission_pickle.py:50-57`` (CPU feature build,
+batch-1 forward). ``BatchedTrajectoryRunner`` produces the same ``{token: Trajectory}`` map with
+the feature building and the forward batched on the GPU:
+
+* agent inputs are loaded per token on the host (a token whose loader raises is reported failed
+  and skipped, like the reference's per-token ``try/except``);
+* features for a batch of up to ``batch_size`` scenes are built by the GPU feature builder in one
+  call per sensor (``features.py``), the forward runs once per batch (numerics-checked);
+* the DDIM start noise is drawn as ONE ``torch.randn(b, 20, 8, 2)`` per batch from the global
+  generator, which yields exactly the values of ``b`` successive per-token ``torch.randn(1, 20, 8,
+  2)`` draws of the reference (transfuser_model_v2.py:593; 320 = 20 x 16 normals per scene keeps
+  PyTorch's 16-wide CPU normal fill aligned - tests/test_runner.py), so a seeded batched run equals a
+  seeded per-token run scene for scene;
+* ``run_distributed`` shards the token list over the ranks of a torch.distributed group (one
+  process per GPU) and gathers the per-rank maps with one ``all_gather_object``.
+
+PDM scoring stays on the CPU (``pdm_score``, out of scope): feed it the returned trajectories.
+"""
+from typing import Callable, Dict, Iterable, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .agent import DiffusionDriveAgent, Trajectory
+from .features import TransfuserFeatureBuilder
+
+
+class BatchedTrajectoryRunner:
+    def __init__(self, agent: DiffusionDriveAgent, batch_size: int = 64, device: Optional[int] = None):
+        if batch_size < 1:
+            raise ValueError("batch_size must be >= 1")
+        self.agent = agent
+        self.batch_size = batch_size
+        self.device = agent._transfuser_model.device if device is None else device
+        self.builder = TransfuserFeatureBuilder(agent._config, device=self.device)
+        self.failed: List[Tuple[str, str]] = []
+
+    def _run_batch(self, tokens: List[str], inputs: List) -> Dict[str, Trajectory]:
+        cfg = self.agent._config
+        feats = self.builder.compute_features_batch(inputs)
+        noise = torch.randn((len(inputs), cfg.num_modes, cfg.trajectory_sampling.num_poses, 2))
+        with torch.no_grad():
+            out = self.agent._transfuser_model.forward(feats, noise=noise, safe=True)
+        poses = out["trajectory"].cpu().numpy()
+        return {t: Trajectory(np.ascontiguousarray(poses[i])) for i, t in enumerate(tokens)}
+
+    def run(self, tokens: Iterable[str], get_agent_input: Callable[[str], object]) -> Dict[str, Trajectory]:
+        """{token: Trajectory} for every token whose input loads; failures land in ``self.failed``."""
+        out: Dict[str, Trajectory] = {}
+        pend_t, pend_i = [], []
+        for tok in tokens:
+            try:
+                ai = get_agent_input(tok)
+            except Exception as e:  # noqa: BLE001 - the reference marks the token invalid and goes on
+                self.failed.append((tok, repr(e)))
+                continue
+            pend_t.append(tok)
+            pend_i.append(ai)
+            if len(pend_t) == self.batch_size:
+                out.update(self._run_batch(pend_t, pend_i))
+                pend_t, pend_i = [], []
+        if pend_t:
+            out.update(self._run_batch(pend_t, pend_i))
+        return out
+
+    def run_distributed(self, tokens: List[str], get_agent_input: Callable[[str], object],
+                        group=None) -> Dict[str, Trajectory]:
+        """Shard ``tokens`` contiguously over the ranks, run locally, gather every rank's map."""
+        import torch.distributed as dist
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        per = (len(tokens) + world - 1) // world
+        local = self.run(tokens[rank * per:(rank + 1) * per], get_agent_input)
+        if world == 1:
+            return local
+        parts: List[Optional[dict]] = [None] * world
+        dist.all_gather_object(parts, {t: tr.poses for t, tr in local.items()}, group=group)
+        merged: Dict[str, Trajectory] = {}
+        for p in parts:
+            merged.update({t: Trajectory(np.asarray(v)) for t, v in p.items()})
+        return merged

@@ -1,0 +1,41 @@
+"""Batched evaluation producer (diffusiondrive_amd/runner.py) vs the per-token reference loop."""
+import numpy as np
+import pytest
+import torch
+
+from test_agent import make_agent_input
+
+
+def test_batched_noise_draw_equals_per_token_draws():
+    """One randn(b, 20, 8, 2) == b successive randn(1, 20, 8, 2) (transfuser_model_v2.py:593)."""
+    torch.manual_seed(123)
+    seq = torch.cat([torch.randn(1, 20, 8, 2) for _ in range(5)])
+    torch.manual_seed(123)
+    bat = torch.randn(5, 20, 8, 2)
+    assert torch.equal(seq, bat)
+
+
+@pytest.mark.gpu
+def test_runner_matches_per_token_compute_trajectory(gpu, seeded_sd):
+    from diffusiondrive_amd.agent import DiffusionDriveAgent
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.runner import BatchedTrajectoryRunner
+    agent = DiffusionDriveAgent(TransfuserConfig(), device=0)
+    agent.load_state_dict(seeded_sd)
+    inputs = {f"tok{i}": make_agent_input(100 + i, n_points=5000 + 1000 * i) for i in range(5)}
+
+    def load(tok):
+        if tok == "bad":
+            raise FileNotFoundError("missing sensor blob")
+        return inputs[tok]
+
+    tokens = ["tok0", "tok1", "bad", "tok2", "tok3", "tok4"]
+    torch.manual_seed(9)
+    runner = BatchedTrajectoryRunner(agent, batch_size=2)
+    got = runner.run(tokens, load)
+    assert set(got) == set(inputs) and [t for t, _ in runner.failed] == ["bad"]
+    torch.manual_seed(9)
+    for tok in ["tok0", "tok1", "tok2", "tok3", "tok4"]:  # the reference's per-token loop
+        ref = agent.compute_trajectory(inputs[tok])
+        l2 = float(np.sqrt(((got[tok].poses[:, :2].astype(np.float64) - ref.poses[:, :2]) ** 2).sum()))
+        assert got[tok].poses.shape == (8, 3) and l2 <= 1e-4, (tok, l2)

@@ -7,6 +7,8 @@
 * C2  batch 64, ResNet-34, 2 truncated DDIM steps: fp32 / f16x3 / bf16 gemm modes.
 * C4  batch 64, ResNet-50 image trunk (nuScenes-style config; LiDAR stays ResNet-34): bf16 (the
       config's dtype) and the fp32-class modes, with the bf16 waypoint deviation from f16x3.
+* C6  end to end from raw sensors: GPU feature builder + forward, raw data resident in HBM and
+      from host memory (PCIe-inclusive), plus the feature build alone.
 * C5  latency curve: truncated DDIM (reference schedule) N = 1..20 steps and vanilla
       (non-truncated, x_T = noise over 1000 train steps) N = 2..20, batch 64, f16x3.
 All inputs synthetic and seeded, weights seeded random (no checkpoint download), inputs resident
@@ -121,6 +123,63 @@ def main():
     print("C5", json.dumps(curve), flush=True)
     m.close()
 
+    # ---- end to end from raw sensors (GPU feature builder + forward), batch 64, f16x3
+    from diffusiondrive_amd import _lib
+    from diffusiondrive_amd.features import camera_features, lidar_features
+    m, feats, noise = setup("resnet34", 64)
+    cfg = m.config
+    r = np.random.default_rng(0)
+    B, NPTS = 64, 100_000
+    imgs = r.integers(0, 256, (B, 3, 1080, 1920, 3), dtype=np.uint8)
+    pcs = [np.stack([r.uniform(-40, 40, NPTS), r.uniform(-40, 40, NPTS), r.uniform(-1, 3, NPTS)]).astype(np.float32)
+           for _ in range(B)]
+    cams_d = torch.from_numpy(imgs).to(dev)
+    offs = torch.from_numpy(np.arange(B + 1, dtype=np.int64) * NPTS).to(dev)
+    xyz_d = torch.from_numpy(np.concatenate([p.reshape(-1) for p in pcs])).to(dev)
+    cam_o = torch.empty((B, 3, 256, 1024), device=dev)
+    lid_o = torch.empty((B, 1, 256, 256), device=dev)
+    lib = _lib.load()
+
+    def build_resident():
+        st = torch.cuda.current_stream().cuda_stream
+        _lib.check(lib.dd_build_camera(cams_d.data_ptr(), B, 1080, 1920, cam_o.data_ptr(), 256, 1024, st), lib, op=True)
+        _lib.check(lib.dd_build_lidar(xyz_d.data_ptr(), offs.data_ptr(), B, 1, lid_o.data_ptr(), 256, -32.0, 32.0, 4,
+                                      100.0, 0.2, 5, NPTS, st), lib, op=True)
+
+    def e2e(resident):
+        if resident:
+            build_resident()
+            f = {"camera_feature": cam_o, "lidar_feature": lid_o, "status_feature": feats["status_feature"]}
+        else:
+            f = {"camera_feature": camera_features([tuple(imgs[b]) for b in range(B)], cfg, 0),
+                 "lidar_feature": lidar_features(pcs, cfg, 0), "status_feature": feats["status_feature"]}
+        return m.forward(f, noise=noise)
+
+    e2e_rows = {}
+    for name, resident in (("raw_sensors_resident_in_hbm", True), ("raw_sensors_from_host_incl_h2d", False)):
+        for _ in range(2):
+            e2e(resident)
+        torch.cuda.synchronize()
+        reps = a.steps if resident else max(2, a.steps // 3)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            e2e(resident)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        e2e_rows[name] = {"ms_per_batch": round(ms, 3), "scenes_per_s": round(B / ms * 1e3, 2)}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        build_resident()
+    torch.cuda.synchronize()
+    fb = (time.perf_counter() - t0) / a.steps * 1e3
+    e2e_rows["feature_build_only_resident"] = {"ms_per_batch": round(fb, 3), "scenes_per_s": round(B / fb * 1e3, 2),
+                                               "raw_bytes_per_scene": int(3 * 1080 * 1920 * 3 + 12 * NPTS)}
+    res["configs"]["C6_end_to_end_raw_sensors_batch64"] = {"gemm": "f16x3", "points_per_scene": NPTS,
+                                                           "rows": e2e_rows}
+    print("C6", json.dumps(e2e_rows), flush=True)
+    m.close()
+
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out + ".json", "w") as f:
         json.dump(res, f, indent=1)
@@ -141,6 +200,10 @@ def main():
               "|---|" + "---|" * 8]
     for sch, cv in curve.items():
         lines.append(f"| {sch} | " + " | ".join(str(cv.get(n, "-")) for n in (1, 2, 4, 5, 6, 8, 10, 20)) + " |")
+    lines += ["", "C6 end to end from raw sensors (3 x 1080x1920 uint8 cameras + 100k LiDAR points per scene), "
+                  "batch 64, f16x3:", "", "| path | ms / batch | scenes/s |", "|---|---|---|"]
+    for k, v in e2e_rows.items():
+        lines.append(f"| {k} | {v['ms_per_batch']} | {v['scenes_per_s']} |")
     with open(a.out + ".md", "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
