@@ -58,7 +58,7 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0, int DBG = 0>
+template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0, int DBG = 0, int SCHED = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 - a 32-wide K chunk lies inside one filter tap, the
@@ -359,9 +359,55 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   // K loop runs to an even count): a conditional load would make hipcc's vmcnt bookkeeping fall
   // back to vmcnt(0) and drain the chunk kept in flight.
   auto iteration = [&](int kc, auto NEXT) {
-    compute(kc & 1);
-    store_chunk((kc + 1) & 1, NEXT);
-    load_chunk(NEXT, (kc + 3) * BK);
+    if constexpr (SCHED == 0 || PREC == 1 || DBG != 0) {
+      compute(kc & 1);
+      store_chunk((kc + 1) & 1, NEXT);
+      load_chunk(NEXT, (kc + 3) * BK);
+    } else {
+      // fragment reads of this chunk first, then the staging of the next chunks, then the MFMAs:
+      // the LDS reads precede the LDS writes in program order (the compiler cannot prove the two
+      // buffers disjoint), and the MFMAs (register-only) are free to interleave with the staging.
+      const char* st = lds + (kc & 1) * STAGE;
+      const char* sah = st;
+      const char* sal = st + BM * ROWB;
+      const char* sbh = st + NIMG * BM * ROWB;
+      const char* sbl = st + (NIMG * BM + BN) * ROWB;
+      half8 ah[2][TM], al[2][TM], bh[2][TN], bl[2][TN];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          bh[s2][j] = *reinterpret_cast<const half8*>(sbh + b_roff[s2][j]);
+          bl[s2][j] = *reinterpret_cast<const half8*>(sbl + b_roff[s2][j]);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          ah[s2][i] = *reinterpret_cast<const half8*>(sah + a_roff[s2][i]);
+          al[s2][i] = *reinterpret_cast<const half8*>(sal + a_roff[s2][i]);
+        }
+      }
+      store_chunk((kc + 1) & 1, NEXT);
+      load_chunk(NEXT, (kc + 3) * BK);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2][i], bh[s2][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2][i], bl[s2][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2][i], bh[s2][j], acc[i][j], 0, 0, 0);
+      }
+      if constexpr (SCHED == 2) __builtin_amdgcn_iglp_opt(0);
+    }
     __syncthreads();
   };
 
@@ -439,6 +485,23 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
   static const int dbg = getenv("DDMI_X3_DBG") ? atoi(getenv("DDMI_X3_DBG")) : 0;
+  static const int sched = getenv("DDMI_X3_SCHED") ? atoi(getenv("DDMI_X3_SCHED")) : 0;
+  if constexpr ((WM == 2 && WN == 2 && TM == 2 && TN == 2) || (WM == 4 && WN == 1 && TM == 2 && TN == 2)) {
+    if (sched && a.prec == 0 && a.Cin % BK == 0 && a.KH * a.KW <= 32) {
+#define DD_SCH(V)                                                                                          \
+  case V:                                                                                                  \
+    hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1, 0, 0, V>), grid, dim3(64 * WM * WN), 0, st, a, M, K, \
+                       ntm, ntn);                                                                          \
+    break;
+      switch (sched) {
+        DD_SCH(1) DD_SCH(2)
+        default: throw std::runtime_error("bad DDMI_X3_SCHED");
+      }
+#undef DD_SCH
+      DD_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   if constexpr (WM == 2 && WN == 2 && TM == 2 && TN == 2) {
     if (dbg && a.prec == 0 && a.Cin % BK == 0 && a.KH * a.KW <= 32) {
 #define DD_DBG(D) \
@@ -466,6 +529,8 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   DD_HIP_CHECK(hipGetLastError());
 }
 
+bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st);  // conv_x5.hip
+
 void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if (a.Cin % 4 != 0) throw std::runtime_error("conv_x3: Cin must be a multiple of 4");
   if ((a.in_sw % 4) || (a.in_sh % 4) || (a.in_sn % 4) || (reinterpret_cast<uintptr_t>(a.in) % 16))
@@ -486,6 +551,10 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
     throw std::runtime_error("conv_x3: operand extent >= 2 GiB (split the batch)");
   if ((int64_t)a.Ho * a.out_sh >= (int64_t(1) << 31) || (int64_t)a.Ho * a.res_sh >= (int64_t(1) << 31))
     throw std::runtime_error("conv_x3: per-image output extent too large");
+  // default f16x3 path: the LDS-DMA kernel (conv_x5.hip) for grids that fill the chip
+  static const int use_x5 = getenv("DDMI_X5") ? atoi(getenv("DDMI_X5")) : 1;
+  if (use_x5 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x5(a, M, K, st))
+    return;
   const int64_t t128 = ((M + 127) / 128) * (int64_t)((a.Cout + 127) / 128);
   const int64_t t256 = ((M + 255) / 256) * (int64_t)((a.Cout + 127) / 128);
   static const int big = getenv("DDMI_X3_BIG") ? atoi(getenv("DDMI_X3_BIG")) : 0;

@@ -1,0 +1,342 @@
+// f16x3 implicit-GEMM conv / GEMM, LDS-DMA edition (the default f16x3 kernel; conv_x3.hip keeps
+// the register-staged variant and the bf16 mode).
+//
+// Same arithmetic as conv_x3.hip (fp32 operands split into fp16 hi + lo, products ah*bh + ah*bl +
+// al*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation; numerics in that file's header), different
+// staging. conv_x3's measured bound is its register-staged operand pipeline: global loads into
+// VGPRs, the split, and ds_writes through the ~80 B/clk VGPR->LDS store path, serialised with the
+// MFMAs. Here both operands go HBM/L2 -> LDS by LDS-DMA (`buffer_load_dwordx4 ... lds`), which
+// bypasses VGPRs and the store path:
+//  * A (fp32 NHWC activations) lands in LDS unsplit as [BM][32] fp32 rows (128 B) whose 16-B slots
+//    are XOR-swizzled by (row >> 1) & 7: the DMA writes lane-linearly, so each lane fetches the
+//    global piece that belongs at its LDS position, and a 16-lane ds_read_b128 group (16 rows, one
+//    logical slot) hits 16 distinct slots of the 256-B bank row - conflict-free.
+//  * The split moves to fragment-read time: each wave converts the 8 fp32 of its A fragment into
+//    half8 hi / lo in registers (v_cvt_pk_f16_f32), ~2 VALU per MFMA, hidden under the MFMAs.
+//  * B (pre-split fp16 hi / lo weight images [N][ldh]) lands as [BN][32] fp16 rows (64 B) per
+//    image, slot swizzle (row >> 2) & 3, read with ds_read_b128 as in conv_x3.
+//  * Conv zero padding and ragged M / N / K edges: out-of-range buffer offsets (>= num_records)
+//    make the DMA deposit zeros; no per-element branches.
+//  * Two LDS stages; one barrier per 32-wide K chunk: wait for this wave's DMAs (vmcnt(0)), barrier
+//    (every wave's DMAs of chunk kc have landed and every wave has finished reading chunk kc-1), issue
+//    chunk kc+1's DMAs into the freed stage, then the chunk-kc MFMAs run while they fly.
+//  * 256 x 256 / 256 x 128 / 256 x 64 tiles (8 / 8 / 4 waves): 64 KB of operands per 32-deep K chunk
+//    feed 384 MFMAs at 256 x 256 - half the L2 bytes per MFMA of conv_x3's 128 x 128.
+//  * XCD-aware bijective tile remap; fused epilogue (per-channel weight scale, alpha, bias,
+//    residual, ReLU, strided NHWC store, non-finite flag) as conv_x3.
+#include <type_traits>
+
+#include "common.h"
+
+namespace ddmi {
+
+namespace {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_v __attribute__((ext_vector_type(2)));
+typedef float float2_v __attribute__((ext_vector_type(2)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int KC = 32;                 // K chunk
+constexpr uint32_t kOOB5 = 0x80000000u;
+
+__device__ inline __amdgpu_buffer_rsrc_t rsrc5(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)kOOB5, 0x00020000);
+}
+
+__device__ inline void dma16(__amdgpu_buffer_rsrc_t r, const char* lds_wave_base, uint32_t byte_off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_wave_base, 16, byte_off, 0, 0, 0);
+}
+
+// 8 fp32 -> hi / lo fp16 fragments (RNE twice)
+__device__ inline void split8(const float4& p, const float4& q, half8_t& hi, half8_t& lo) {
+  const float x[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const half2_v h = __builtin_convertvector((float2_v){x[e], x[e + 1]}, half2_v);
+    const float2_v f = __builtin_convertvector(h, float2_v);
+    const half2_v l = __builtin_convertvector((float2_v){x[e] - f.x, x[e + 1] - f.y}, half2_v);
+    hi[e] = h.x;
+    hi[e + 1] = h.y;
+    lo[e] = l.x;
+    lo[e + 1] = l.y;
+  }
+}
+
+}  // namespace
+
+template <int WM, int WN, int TM, int TN, int MODE>
+__global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M, int K, int n_tiles_m,
+                                                               int n_tiles_n) {
+  // MODE 1: Cin % 32 == 0 and KH*KW <= 32 (scalar tap walk, per-row tap masks); MODE 0: generic K.
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int AB = BM * KC * 4;     // A stage bytes (fp32 rows of 128 B)
+  constexpr int BB = BN * KC * 2;     // one B image (fp16 rows of 64 B)
+  constexpr int STAGE = AB + 2 * BB;
+  constexpr int A_IN = BM / 8 / NW;   // A DMA instructions per wave per chunk (8 rows x 128 B each)
+  constexpr int B_IN = BN / 16 / NW;  // B DMA instructions per wave per chunk and image (16 rows x 64 B)
+  static_assert(A_IN >= 1 && BM % (8 * NW) == 0, "A rows per wave");
+  static_assert(B_IN >= 1 && BN % (16 * NW) == 0, "B rows per wave");
+  __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int nblk = n_tiles_m * n_tiles_n;
+  const int bid = blockIdx.x;
+  int tile = bid;
+  if (nblk >= 16) {
+    const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int mt_idx = tile / n_tiles_n;
+  const int nt_idx = tile - mt_idx * n_tiles_n;
+  const int m0 = mt_idx * BM;
+  const int n0 = nt_idx * BN;
+
+  const __amdgpu_buffer_rsrc_t rin = rsrc5(a.in);
+  const __amdgpu_buffer_rsrc_t rwh = rsrc5(a.wh);
+  const __amdgpu_buffer_rsrc_t rwl = rsrc5(a.wl);
+  const int in_sh = (int)a.in_sh, in_sw = (int)a.in_sw;
+  const int ldh = (int)a.ldh;
+  const int Kp = (K + 7) & ~7;
+
+  // ---- A DMA lanes: instruction q of this wave fills rows ar0 + q*8 .. +7; lane -> (row, LDS slot)
+  const int a_rbase = wave * A_IN * 8;
+  int abase[A_IN], aih0[A_IN], aiw0[A_IN], akq[A_IN];
+  uint32_t amask[A_IN];
+#pragma unroll
+  for (int q = 0; q < A_IN; ++q) {
+    const int r = a_rbase + q * 8 + (lane >> 3);
+    akq[q] = (lane & 7) ^ ((r >> 1) & 7);  // logical 16-B slot (4 channels) this lane fetches
+    const int m = m0 + r;
+    const bool v = m < M;
+    const int mm = v ? m : 0;
+    const int ow = mm % a.Wo;
+    const int t2 = mm / a.Wo;
+    const int oh = t2 % a.Ho;
+    const int n = t2 / a.Ho;
+    const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+    if constexpr (MODE == 1) {
+      abase[q] = n * (int)a.in_sn + ih0 * in_sh + iw0 * in_sw + akq[q] * 4;
+      uint32_t mk = 0;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+            mk |= 1u << (kh * a.KW + kw);
+      amask[q] = v ? mk : 0u;
+    } else {
+      abase[q] = n * (int)a.in_sn;
+      aih0[q] = v ? ih0 : -(1 << 28);
+      aiw0[q] = iw0;
+    }
+  }
+  // ---- B DMA lanes: instruction q fills rows b_rbase + q*16 .. +15 of each image
+  const int b_rbase = wave * B_IN * 16;
+  uint32_t boff[B_IN];
+  bool bok[B_IN];
+  int bkb[B_IN];
+#pragma unroll
+  for (int q = 0; q < B_IN; ++q) {
+    const int c = b_rbase + q * 16 + (lane >> 2);
+    const int slot = (lane & 3) ^ ((c >> 2) & 3);
+    const int n = n0 + c;
+    bok[q] = n < a.Cout;
+    bkb[q] = slot * 8;
+    boff[q] = (uint32_t)(n * ldh + slot * 8) * 2u;
+  }
+
+  int t_tap = 0, t_ci = 0, t_kw = 0, t_off = 0;  // MODE 1 scalar tap walk (chunk order)
+  auto issue = [&](int buf, int k0) {
+    char* st = lds + buf * STAGE;
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int q = 0; q < A_IN; ++q) {
+        const bool ok = t_tap < 32 && ((amask[q] >> (t_tap & 31)) & 1u);
+        dma16(rin, st + (a_rbase + q * 8) * 128, ok ? (uint32_t)(abase[q] + t_off) * 4u : kOOB5);
+      }
+      t_ci += KC;
+      t_off += KC;
+      if (t_ci == a.Cin) {
+        t_ci = 0;
+        ++t_tap;
+        t_off += in_sw - a.Cin;
+        if (++t_kw == a.KW) {
+          t_kw = 0;
+          t_off += in_sh - a.KW * in_sw;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < A_IN; ++q) {
+        const int kk = k0 + akq[q] * 4;
+        const int tap = kk / a.Cin;
+        const int ci = kk - tap * a.Cin;
+        const int kh = tap / a.KW;
+        const int kw = tap - kh * a.KW;
+        const int ih = aih0[q] + kh, iw = aiw0[q] + kw;
+        const bool ok = kk < K && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        dma16(rin, st + (a_rbase + q * 8) * 128, ok ? (uint32_t)(abase[q] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB5);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B_IN; ++q) {
+      const uint32_t off = (bok[q] && k0 + bkb[q] < Kp) ? boff[q] + (uint32_t)k0 * 2u : kOOB5;
+      dma16(rwh, st + AB + (b_rbase + q * 16) * 64, off);
+      dma16(rwl, st + AB + BB + (b_rbase + q * 16) * 64, off);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, hh = lane >> 5;
+  f32x16_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // fragment read offsets per k16 step s2: A fp32 logical slots 4*s2 + 2*hh, +1; B slot 2*s2 + hh
+  int a_ro[2][TM][2], b_ro[2][TN];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = (wm * TM + i) * 32 + li;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) a_ro[s2][i][u] = r * 128 + (((4 * s2 + 2 * hh + u) ^ ((r >> 1) & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = (wn * TN + j) * 32 + li;
+      b_ro[s2][j] = AB + c * 64 + (((2 * s2 + hh) ^ ((c >> 2) & 3)) << 4);
+    }
+  }
+
+  const int nk = (K + KC - 1) / KC;
+  issue(0, 0);
+  for (int kc = 0; kc < nk; ++kc) {
+    __syncthreads();  // (vmcnt(0) first: LDS-DMA is outstanding) chunk kc landed; stage (kc+1)&1 is free
+    issue((kc + 1) & 1, (kc + 1) * KC);
+    const char* st = lds + (kc & 1) * STAGE;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      half8_t ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = *reinterpret_cast<const half8_t*>(st + b_ro[s2][j]);
+        bl[j] = *reinterpret_cast<const half8_t*>(st + b_ro[s2][j] + BB);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float4 p = *reinterpret_cast<const float4*>(st + a_ro[s2][i][0]);
+        const float4 q = *reinterpret_cast<const float4*>(st + a_ro[s2][i][1]);
+        split8(p, q, ah[i], al[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // drain the trailing (all-OOB) DMA before the block retires
+
+  // ---- fused epilogue (as conv_x3). C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  bool bad = false;
+  float scl_v[TN], bias_v[TN];
+  int ncol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    ncol[j] = n0 + (wn * TN + j) * 32 + li;
+    const bool nv = ncol[j] < a.Cout;
+    bias_v[j] = (a.bias && nv) ? a.bias[ncol[j]] : 0.f;
+    scl_v[j] = nv ? a.wsinv[ncol[j]] * a.alpha : 0.f;
+  }
+  float* out = a.out;
+  const float* res = a.res;
+  const int osh = (int)a.out_sh, osw = (int)a.out_sw;
+  const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mbase = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh;
+      int ow = mbase % a.Wo;
+      int t2 = mbase / a.Wo;
+      int oh = t2 % a.Ho;
+      int n = t2 / a.Ho;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = mbase + e;
+        if (m < M) {
+          float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
+          const float* rrow = res ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if (ncol[j] < a.Cout) {
+              const float acc_v = acc[i][j][q * 4 + e];
+              bad |= !__builtin_isfinite(acc_v);
+              float v = acc_v * scl_v[j] + bias_v[j];
+              if (rrow) v += rrow[ncol[j]];
+              if (a.relu) v = fmaxf(v, 0.f);
+              orow[ncol[j]] = v;
+            }
+          }
+        }
+        if (++ow == a.Wo) {
+          ow = 0;
+          if (++oh == a.Ho) {
+            oh = 0;
+            ++n;
+          }
+        }
+      }
+    }
+  }
+  if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+}
+
+template <int WM, int WN, int TM, int TN>
+static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  const int ntm = (M + BM - 1) / BM;
+  const int ntn = (a.Cout + BN - 1) / BN;
+  dim3 grid(ntm * ntn, 1, 1);
+  if (a.Cin % KC == 0 && a.KH * a.KW <= 32)
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+  else
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
+// Returns false when the shape is better served by conv_x3 (small grids).
+bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
+  const int64_t m256 = (M + 255) / 256;
+  if (a.Cout <= 64) {
+    if (m256 < 256) return false;
+    launch_x5_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64, 4 waves
+  } else if (a.Cout <= 128) {
+    if (m256 < 256) return false;
+    launch_x5_cfg<4, 2, 2, 2>(a, M, K, st);  // 256 x 128, 8 waves
+  } else {
+    if (m256 * ((a.Cout + 255) / 256) < 256) return false;
+    launch_x5_cfg<4, 2, 2, 4>(a, M, K, st);  // 256 x 256, 8 waves
+  }
+  return true;
+}
+
+}  // namespace ddmi

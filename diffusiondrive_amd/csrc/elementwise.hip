@@ -41,73 +41,73 @@ void launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int H, int W
 }
 
 // ---------------------------------------------------------------- maxpool 3x3 s2 p1 (timm stem)
-__global__ void maxpool_kernel(const float4* __restrict__ in, float4* __restrict__ out, int B, int H, int W,
-                               int C4, int Ho, int Wo) {
-  const int64_t n = (int64_t)B * Ho * Wo * C4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = i % C4;
-    int64_t t = i / C4;
-    const int ox = t % Wo;
-    t /= Wo;
-    const int oy = t % Ho;
-    const int64_t b = t / Ho;
+// One block row per output row (blockIdx.z = b, blockIdx.y = oy): 32-bit index math, float4 channel vectors along x.
+__global__ void maxpool_kernel(const float4* __restrict__ in, float4* __restrict__ out, int H, int W, int C4,
+                               int Ho, int Wo) {
+  const int b = blockIdx.z, oy = blockIdx.y;
+  const int row = b * Ho + oy;
+  const int n = Wo * C4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int ox = i / C4, c = i - ox * C4;
     float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
       const int y = oy * 2 - 1 + dy;
       if ((unsigned)y >= (unsigned)H) continue;
+      const float4* rowp = in + ((size_t)b * H + y) * W * C4 + c;
+#pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const int x = ox * 2 - 1 + dx;
         if ((unsigned)x >= (unsigned)W) continue;
-        const float4 v = in[((b * H + y) * W + x) * C4 + c];
+        const float4 v = rowp[(size_t)x * C4];
         m.x = fmaxf(m.x, v.x);
         m.y = fmaxf(m.y, v.y);
         m.z = fmaxf(m.z, v.z);
         m.w = fmaxf(m.w, v.w);
       }
     }
-    out[i] = m;
+    out[(size_t)row * n + i] = m;
   }
 }
 
 void launch_maxpool3x3s2(const float* in, float* out, int B, int H, int W, int C, int Ho, int Wo,
                          hipStream_t st) {
   if (C % 4) throw std::runtime_error("maxpool: C % 4 != 0");
-  const int64_t n = (int64_t)B * Ho * Wo * (C / 4);
-  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(n)), dim3(256), 0, st, reinterpret_cast<const float4*>(in),
-                     reinterpret_cast<float4*>(out), B, H, W, C / 4, Ho, Wo);
+  const int n = Wo * (C / 4);
+  dim3 grid((n + 255) / 256, Ho, B);
+  hipLaunchKernelGGL(maxpool_kernel, grid, dim3(256), 0, st, reinterpret_cast<const float4*>(in),
+                     reinterpret_cast<float4*>(out), H, W, C / 4, Ho, Wo);
   DD_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------- adaptive avg pool (exact windows)
-// transfuser_backbone.py:47-58,249-250: windows divide exactly at every scale.
-__global__ void avgpool_kernel(const float* __restrict__ in, int B, int H, int W, int C, int oh, int ow,
-                               View4 out, const float* __restrict__ add) {
+// transfuser_backbone.py:47-58,249-250: windows divide exactly at every scale. One block row per
+// output row (b, y), threads over (x, c); the window sum runs in the reference's (dy, dx) order.
+__global__ void avgpool_kernel(const float* __restrict__ in, int H, int W, int C, int oh, int ow, View4 out,
+                               const float* __restrict__ add) {
   const int kh = H / oh, kw = W / ow;
   const float inv = 1.0f / (float)(kh * kw);
-  const int64_t n = (int64_t)B * oh * ow * C;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = i % C;
-    int64_t t = i / C;
-    const int x = t % ow;
-    t /= ow;
-    const int y = t % oh;
-    const int64_t b = t / oh;
+  const int b = blockIdx.z, y = blockIdx.y;
+  const int n = ow * C;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int x = i / C, c = i - x * C;
     float s = 0.f;
     for (int dy = 0; dy < kh; ++dy) {
-      const float* row = in + ((b * H + (int64_t)y * kh + dy) * W + (int64_t)x * kw) * C + c;
-      for (int dx = 0; dx < kw; ++dx) s += row[(int64_t)dx * C];
+      const float* r = in + (((size_t)b * H + (size_t)y * kh + dy) * W + (size_t)x * kw) * C + c;
+      for (int dx = 0; dx < kw; ++dx) s += r[(size_t)dx * C];
     }
     float v = s * inv;
-    if (add) v += add[((int64_t)y * ow + x) * C + c];
-    out.p[b * out.sn + y * out.sh + x * out.sw + c * out.sc] = v;
+    if (add) v += add[((size_t)y * ow + x) * C + c];
+    out.p[(int64_t)b * out.sn + (int64_t)y * out.sh + (int64_t)x * out.sw + (int64_t)c * out.sc] = v;
   }
 }
 
 void launch_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow, View4 out, const float* add,
                     hipStream_t st) {
   if (H % oh || W % ow) throw std::runtime_error("avgpool: non-integer window");
-  const int64_t n = (int64_t)B * oh * ow * C;
-  hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(n)), dim3(256), 0, st, in, B, H, W, C, oh, ow, out, add);
+  const int n = ow * C;
+  dim3 grid((n + 255) / 256, oh, B);
+  hipLaunchKernelGGL(avgpool_kernel, grid, dim3(256), 0, st, in, H, W, C, oh, ow, out, add);
   DD_HIP_CHECK(hipGetLastError());
 }
 
@@ -123,36 +123,75 @@ __device__ inline void bl_index(int dst, float ratio, int in_size, int& i0, int&
   l0 = 1.f - l1;
 }
 
-__global__ void bilinear_kernel(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float rh,
-                                float rw, int accumulate) {
-  const int64_t n = (int64_t)B * Ho * Wo * C;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = i % C;
-    int64_t t = i / C;
-    const int x = t % Wo;
-    t /= Wo;
-    const int y = t % Ho;
-    const int64_t b = t / Ho;
-    int y0, y1, x0, x1;
-    float ly0, ly1, lx0, lx1;
-    bl_index(y, rh, Hi, y0, y1, ly0, ly1);
+// One block row per output row (b, y) (the y taps are block-uniform); threads over (x, channel
+// vector). VEC = 4: float4 channel vectors (unit channel stride, 16-B aligned rows); VEC = 1: any
+// strides. Same arithmetic order as the scalar form (fp-contract off for this file).
+template <int VEC>
+__global__ void bilinear_kernel(View4 in, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float rh, float rw,
+                                int accumulate) {
+  const int b = blockIdx.z, y = blockIdx.y;
+  int y0, y1;
+  float ly0, ly1;
+  bl_index(y, rh, Hi, y0, y1, ly0, ly1);
+  const int CV = C / VEC;
+  const int n = Wo * CV;
+  const float* base = in.p + (int64_t)b * in.sn;
+  float* obase = out.p + (int64_t)b * out.sn + (int64_t)y * out.sh;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int x = i / CV, cv = i - x * CV;
+    int x0, x1;
+    float lx0, lx1;
     bl_index(x, rw, Wi, x0, x1, lx0, lx1);
-    const float* base = in.p + b * in.sn + (int64_t)c * in.sc;
-    const float v00 = base[y0 * in.sh + x0 * in.sw];
-    const float v01 = base[y0 * in.sh + x1 * in.sw];
-    const float v10 = base[y1 * in.sh + x0 * in.sw];
-    const float v11 = base[y1 * in.sh + x1 * in.sw];
-    const float v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
-    float* o = out.p + b * out.sn + (int64_t)y * out.sh + (int64_t)x * out.sw + (int64_t)c * out.sc;
-    *o = accumulate ? (*o + v) : v;
+    if constexpr (VEC == 4) {
+      const int c = cv * 4;
+      const float4 v00 = *reinterpret_cast<const float4*>(base + y0 * in.sh + x0 * in.sw + c);
+      const float4 v01 = *reinterpret_cast<const float4*>(base + y0 * in.sh + x1 * in.sw + c);
+      const float4 v10 = *reinterpret_cast<const float4*>(base + y1 * in.sh + x0 * in.sw + c);
+      const float4 v11 = *reinterpret_cast<const float4*>(base + y1 * in.sh + x1 * in.sw + c);
+      float4 v;
+      v.x = ly0 * (lx0 * v00.x + lx1 * v01.x) + ly1 * (lx0 * v10.x + lx1 * v11.x);
+      v.y = ly0 * (lx0 * v00.y + lx1 * v01.y) + ly1 * (lx0 * v10.y + lx1 * v11.y);
+      v.z = ly0 * (lx0 * v00.z + lx1 * v01.z) + ly1 * (lx0 * v10.z + lx1 * v11.z);
+      v.w = ly0 * (lx0 * v00.w + lx1 * v01.w) + ly1 * (lx0 * v10.w + lx1 * v11.w);
+      float4* o = reinterpret_cast<float4*>(obase + (int64_t)x * out.sw + c);
+      if (accumulate) {
+        const float4 p = *o;
+        v.x = p.x + v.x;
+        v.y = p.y + v.y;
+        v.z = p.z + v.z;
+        v.w = p.w + v.w;
+      }
+      *o = v;
+    } else {
+      const int c = cv;
+      const float* cb = base + (int64_t)c * in.sc;
+      const float v00 = cb[y0 * in.sh + x0 * in.sw];
+      const float v01 = cb[y0 * in.sh + x1 * in.sw];
+      const float v10 = cb[y1 * in.sh + x0 * in.sw];
+      const float v11 = cb[y1 * in.sh + x1 * in.sw];
+      const float v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+      float* o = obase + (int64_t)x * out.sw + (int64_t)c * out.sc;
+      *o = accumulate ? (*o + v) : v;
+    }
   }
 }
 
 void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float ratio_h,
                      float ratio_w, int accumulate, hipStream_t st) {
-  const int64_t n = (int64_t)B * Ho * Wo * C;
-  hipLaunchKernelGGL(bilinear_kernel, dim3(grid_for(n)), dim3(256), 0, st, in, B, Hi, Wi, C, out, Ho, Wo,
-                     ratio_h, ratio_w, accumulate);
+  if (Ho > 65535 || B > 65535) throw std::runtime_error("bilinear: Ho / B > 65535");
+  if ((int64_t)Hi * in.sh >= (int64_t(1) << 31) || (int64_t)Wo * out.sw >= (int64_t(1) << 31))
+    throw std::runtime_error("bilinear: per-image extent too large");
+  const bool vec = C % 4 == 0 && in.sc == 1 && out.sc == 1 && in.sh % 4 == 0 && in.sw % 4 == 0 &&
+                   in.sn % 4 == 0 && out.sh % 4 == 0 && out.sw % 4 == 0 && out.sn % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(in.p) % 16 == 0 && reinterpret_cast<uintptr_t>(out.p) % 16 == 0;
+  const int n = Wo * (vec ? C / 4 : C);
+  dim3 grid((n + 255) / 256, Ho, B);
+  if (vec)
+    hipLaunchKernelGGL(bilinear_kernel<4>, grid, dim3(256), 0, st, in, Hi, Wi, C, out, Ho, Wo, ratio_h, ratio_w,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(bilinear_kernel<1>, grid, dim3(256), 0, st, in, Hi, Wi, C, out, Ho, Wo, ratio_h, ratio_w,
+                       accumulate);
   DD_HIP_CHECK(hipGetLastError());
 }
 

@@ -80,6 +80,13 @@ def test_conv2d(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     (2, 64, 80, 64, 64, 3, 1, 1, True, False),    # Cout 64, 256-row tiles
     (1, 48, 64, 128, 256, 3, 1, 1, False, True),  # 128x128 tiles
     (1, 9, 11, 36, 24, 3, 1, 1, False, False),    # Cin % 32 != 0, K tail
+    # grids that fill the chip take the LDS-DMA kernel (conv_x5.hip)
+    (16, 64, 64, 64, 64, 3, 1, 1, True, True),    # 256 x 64 tiles, tap walk, padding via OOB DMA
+    (4, 128, 128, 32, 128, 3, 1, 1, True, False), # 256 x 128 tiles, Cin = 32
+    (1, 256, 256, 128, 256, 1, 1, 0, False, True),# 256 x 256 tiles, 1x1
+    (16, 64, 64, 36, 200, 3, 1, 1, True, False),  # generic K path, ragged N in a 256-wide tile
+    (1, 518, 518, 4, 64, 7, 2, 3, True, False),   # stem geometry (7x7/s2 on 4 padded channels)
+    (3, 90, 250, 64, 256, 3, 2, 1, False, False), # stride 2, ragged M
 ])
 def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     """f16x3 split-MFMA conv vs PyTorch-CPU fp32 (tolerance: fp32-class, 3e-5 of max|ref|)."""
