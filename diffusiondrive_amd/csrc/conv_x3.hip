@@ -530,6 +530,7 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 }
 
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st);  // conv_x5.hip
+bool launch_conv_x6(const ConvArgs& a, hipStream_t st);                 // conv_x6.hip
 
 void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if (a.Cin % 4 != 0) throw std::runtime_error("conv_x3: Cin must be a multiple of 4");
@@ -551,7 +552,10 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
     throw std::runtime_error("conv_x3: operand extent >= 2 GiB (split the batch)");
   if ((int64_t)a.Ho * a.out_sh >= (int64_t(1) << 31) || (int64_t)a.Ho * a.res_sh >= (int64_t(1) << 31))
     throw std::runtime_error("conv_x3: per-image output extent too large");
-  // default f16x3 path: the LDS-DMA kernel (conv_x5.hip) for grids that fill the chip
+  // default f16x3 path: 3x3 stride-1 convs on the halo-reuse direct kernel (conv_x6.hip), other
+  // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
+  static const int use_x6 = getenv("DDMI_X6") ? atoi(getenv("DDMI_X6")) : 1;
+  if (use_x6 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x6(a, st)) return;
   static const int use_x5 = getenv("DDMI_X5") ? atoi(getenv("DDMI_X5")) : 1;
   if (use_x5 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x5(a, M, K, st))
     return;

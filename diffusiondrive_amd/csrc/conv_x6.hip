@@ -1,0 +1,495 @@
+// f16x3 direct 3x3 convolution (stride 1, pad 1) with halo reuse - the default kernel for every
+// 3x3 stride-1 conv of the path: the ResNet-34 BasicBlocks of both trunks (transfuser_backbone.py
+// :23-33, timm BasicBlock conv1/conv2), the FPN up-convs (:124-159) and the decoder's value_proj
+// (modules/blocks.py:68-76,114).
+//
+// Arithmetic: exactly conv_x3.hip's f16x3 (fp32 operand = fp16 hi + lo, products ah*bh + ah*bl +
+// al*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation; numerics and range in that file's header;
+// non-finite accumulators raise DD_NUM_F16_OVERFLOW).
+//
+// Why a direct kernel: the implicit GEMM (conv_x3 / conv_x5) fetches every input pixel once per
+// filter tap, 9x; with f16x3's 4 B per operand element that needs 21-53 B/clk per CU at full MFMA
+// rate - above what a CU takes in from L2 (~30 B/clk, MI355X_MICROARCH.md "Indexed rows"). Here a
+// workgroup owns a TH x TW output tile (256 pixels of one image) x BN output channels and walks
+// K as (32-channel chunk c) x (9 taps):
+//  * A: the (TH+2) x (TW+2) input halo of chunk c is fetched ONCE (register-staged 16-B buffer
+//    loads, OOB offsets give the zero padding), split into hi / lo fp16 in registers, and written
+//    to LDS as 128-B pixel rows [hi 32 | lo 32 halfs]. The 9 taps then read their A fragments from
+//    the same halo at a (kh, kw) shift. Halo double buffered: chunk c+1's halo is loaded during
+//    chunk c's taps and written into the other buffer at its last tap.
+//  * B: pre-split weight images [Cout][ldh] (K order kh, kw, ci) stream through a 3-slot LDS ring,
+//    one slot per (chunk, tap) step, by LDS-DMA (`buffer_load_dwordx4 ... lds`), two steps ahead.
+//  * Per step: one s_waitcnt vmcnt(N) with the exact count of younger memory ops, one barrier.
+//    Every vector-memory op of the main loop is inline asm, so the compiler's waitcnt pass (which
+//    cannot tell an LDS-DMA target from the buffer being read and drains vmcnt(0) before every
+//    ds_read - what serialised conv_x5) never sees them; the counts are derived in the kernel.
+//  * LDS banking: A rows are 128 B; the 16-B slot is XOR-swizzled by (hx >> 1) & 7 of the halo
+//    column, so each 16-lane ds_read_b128 group (output pixels x..x+15 of one or two tile rows,
+//    shifted by kw) hits 16 distinct (row parity, slot) pairs: conflict-free for every tap. B rows
+//    are 64 B per image, slot ^ (n >> 2) & 3 as in conv_x3.
+//  * Traffic per step (BN = 128): B 16 KB + A 41.5 KB / 9 = 21 KB per 1536 MFMA cycles = 13.5
+//    B/clk per CU (implicit GEMM at 256 x 128: 32 B/clk).
+//  * 8 waves (4 x 2), wave tile 64 x (BN / 2); one workgroup per CU (132-136 KB LDS).
+//  * Fused epilogue as conv_x3 (per-channel weight scale, alpha, bias, residual, ReLU, strided NHWC).
+#include <type_traits>
+
+#include "common.h"
+
+namespace ddmi {
+
+namespace {
+
+typedef _Float16 x6h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 x6h2 __attribute__((ext_vector_type(2)));
+typedef float x6f2 __attribute__((ext_vector_type(2)));
+typedef float x6f4 __attribute__((ext_vector_type(4)));
+typedef float x6f16 __attribute__((ext_vector_type(16)));
+typedef int x6i4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kOOB6 = 0x80000000u;
+
+__device__ inline x6i4 rsrc6(const void* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  x6i4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xffffu);  // stride 0
+  r.z = (int)kOOB6;                             // num_records: offsets >= 2^31 read as zero
+  r.w = 0x00020000;
+  return r;
+}
+
+// 16 B per lane from global (buffer offset voff) into LDS at m0 + 16 * lane (m0 = wave base).
+__device__ inline void dma6(x6i4 rsrc, uint32_t lds_wave, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds_wave), "v"(voff), "s"(rsrc)
+               : "memory");
+}
+
+__device__ inline x6f4 vload6(x6i4 rsrc, uint32_t voff) {
+  x6f4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
+  return v;
+}
+
+// wait until at most N vector-memory ops of this wave are outstanding, then LDS ops, then barrier
+template <int N>
+__device__ inline void step_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int N>
+__device__ inline void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ inline void split4(const x6f4 v, uint2& hi, uint2& lo) {
+  const x6h2 h01 = __builtin_convertvector((x6f2){v.x, v.y}, x6h2);
+  const x6h2 h23 = __builtin_convertvector((x6f2){v.z, v.w}, x6h2);
+  const x6f2 f01 = __builtin_convertvector(h01, x6f2);
+  const x6f2 f23 = __builtin_convertvector(h23, x6f2);
+  const x6h2 l01 = __builtin_convertvector((x6f2){v.x - f01.x, v.y - f01.y}, x6h2);
+  const x6h2 l23 = __builtin_convertvector((x6f2){v.z - f23.x, v.w - f23.y}, x6h2);
+  hi = make_uint2(__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23));
+  lo = make_uint2(__builtin_bit_cast(uint32_t, l01), __builtin_bit_cast(uint32_t, l23));
+}
+
+// Does a halo issue (at tap TA of some chunk) fall in the D steps before step t, i.e. after the B
+// DMAs of step t were issued (D steps earlier, ahead of that step's halo)? For the first chunk the
+// window stops at step 0 (the prologue issued chunk 0's halo before every B DMA).
+constexpr bool halo_in_window(int t, int D, int TA, bool first) {
+  for (int j = 1; j <= D; ++j) {
+    const int u = t - j;
+    if (first && u < 0) return false;
+    if (((u % 9) + 9) % 9 == TA) return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+// TH x TW output pixels x BN channels per workgroup of WM x WN waves; B ring of NSLOT slots filled
+// D steps ahead (NSLOT >= D + 1).
+// DBG (timing experiments only, results wrong): 1 no MFMA, 2 no B DMA, 4 no halo, 8 no fragment
+// reads, 16 no per-step barrier.
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int DBG = 0>
+__global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
+                                                               int ntn, int nchunks) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int BM = TH * TW;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM && TN * WN * 32 == BN, "wave tiling");
+  static_assert(NSLOT >= D + 1 && D >= 1 && D <= 8, "ring");
+  constexpr int P = TW + 2;                 // halo row pitch (pixels); even
+  constexpr int HP = (TH + 2) * P;          // halo pixels
+  constexpr int ABYTES = HP * 128;          // one split halo buffer
+  constexpr int BIMG = BN * 64;             // one B image of one ring slot
+  constexpr int BSLOT = 2 * BIMG;
+  constexpr int BQ = BN / 16;               // DMA instructions per image per step
+  constexpr int BPS = 2 * BQ / NW;          // per wave per step
+  static_assert(BPS >= 1 && (2 * BQ) % NW == 0 && BQ % BPS == 0, "B DMA split over the waves");
+  constexpr int ALD = (HP * 8 + NT - 1) / NT;  // halo float4 loads per thread per chunk
+  constexpr int TA = 1;                        // tap step at which the next chunk's halo is issued
+  constexpr int B_OFF = 2 * ABYTES;
+  constexpr int LDS_MAIN = 2 * ABYTES + NSLOT * BSLOT, LDS_EPI = BM * BN * 4;
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
+  const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // ---- tile (XCD-aware bijective remap: each XCD takes a contiguous run of tiles, N-tile major)
+  const int nblk = n_sp * ntn;
+  int tile = blockIdx.x;
+  if (nblk >= 16) {
+    const int q = nblk / 8, r = nblk % 8, x = tile % 8;
+    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+  }
+  const int nt_idx = tile / n_sp;
+  const int sp = tile - nt_idx * n_sp;
+  const int txi = sp % tiles_x;
+  const int t2 = sp / tiles_x;
+  const int tyi = t2 % tiles_y;
+  const int nimg = t2 / tiles_y;
+  const int oy0 = tyi * TH, ox0 = txi * TW;
+  const int n0 = nt_idx * BN;
+  const int Cin = a.Cin;
+
+  const x6i4 rin = rsrc6(a.in);
+
+  // ---- halo staging: thread element e = tid + NT i -> halo pixel e >> 3, channels 4 (e & 7) ..
+  int hofs[ALD];  // element offset of (pixel, 4q) at chunk 0, or -1 (zero fill)
+  int hwad[ALD];  // LDS byte offset (in a halo buffer) of the hi 8 bytes, -1 = no write
+#pragma unroll
+  for (int i = 0; i < ALD; ++i) {
+    const int e = tid + NT * i;
+    const int px = e >> 3, q = e & 7;
+    const int hy = px / P, hx = px - (px / P) * P;
+    const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+    const bool in = px < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    hofs[i] = in ? (int)(nimg * a.in_sn + iy * a.in_sh + ix * a.in_sw) + 4 * q : -1;
+    hwad[i] = px < HP ? px * 128 + ((((q >> 1) ^ (hx >> 1)) & 7) << 4) + ((q & 1) << 3) : -1;
+  }
+  x6f4 hr[ALD];
+  auto halo_issue = [&](int c) {
+    if constexpr (DBG & 4) return;
+    const bool cv = c < nchunks;
+    const int co = c * 32;
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) hr[i] = vload6(rin, (cv && hofs[i] >= 0) ? (uint32_t)(hofs[i] + co) * 4u : kOOB6);
+  };
+  auto halo_tie = [&]() {  // after a wait: no use of the staged registers may move above it
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) asm volatile("" : "+v"(hr[i]));
+  };
+  auto halo_store = [&](int buf) {
+    if constexpr (DBG & 4) return;
+    char* base = lds + buf * ABYTES;
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+      if (hwad[i] < 0) continue;
+      uint2 hi, lo;
+      split4(hr[i], hi, lo);
+      *reinterpret_cast<uint2*>(base + hwad[i]) = hi;
+      *reinterpret_cast<uint2*>(base + (hwad[i] ^ 64)) = lo;
+    }
+  };
+
+  // ---- B ring DMA: wave instruction j covers one image, rows rb .. rb+15 of the slot
+  uint32_t boff[BPS];
+  bool bok[BPS];
+  int brow[BPS];
+#pragma unroll
+  for (int j = 0; j < BPS; ++j) {
+    const int qi = wave * BPS + j;
+    const int rb = (qi % BQ) * 16;
+    const int c = rb + (lane >> 2);
+    const int ls = (lane & 3) ^ ((c >> 2) & 3);
+    const int n = n0 + c;
+    bok[j] = n < a.Cout;
+    boff[j] = (uint32_t)(n * (int)a.ldh + ls * 8) * 2u;
+    brow[j] = rb;
+  }
+  const bool bimg_lo = (wave * BPS) / BQ == 1;
+  const x6i4 rwb = rsrc6(bimg_lo ? (const void*)a.wl : (const void*)a.wh);
+  auto b_issue = [&](int slot, int tap, int c) {
+    if constexpr (DBG & 2) return;
+    const bool cv = c < nchunks;
+    const uint32_t kb = (uint32_t)(tap * Cin + c * 32) * 2u;
+#pragma unroll
+    for (int j = 0; j < BPS; ++j) {
+      const uint32_t dst = lds_u32 + B_OFF + slot * BSLOT + (bimg_lo ? BIMG : 0) + brow[j] * 64;
+      dma6(rwb, __builtin_amdgcn_readfirstlane(dst), (cv && bok[j]) ? boff[j] + kb : kOOB6);
+    }
+  };
+
+  // ---- fragment addresses
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, hh = lane >> 5;
+  int aad[TM][3];  // A (hi, k16 step 0) byte offset in a halo buffer for tap (0, kw)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = (wm * TM + i) * 32 + li;
+    const int y = m / TW, x = m % TW;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) aad[i][kw] = (y * P + x + kw) * 128 + (((hh ^ ((x + kw) >> 1)) & 7) << 4);
+  }
+  int bad_[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c = (wn * TN + j) * 32 + li;
+    bad_[j] = c * 64 + (((hh ^ (c >> 2)) & 3) << 4);
+  }
+
+  x6f16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // fragments of one k16 half-step: F0 = (step, s2 = 0), F1 = (step, s2 = 1)
+  struct Frag {
+    x6h8 ah[TM], al[TM], bh[TN], bl[TN];
+  };
+  Frag F0, F1;
+  auto load_frag = [&](Frag& F, int slot, int c, auto TAP, auto S2) {
+    constexpr int t = decltype(TAP)::value, s2 = decltype(S2)::value;
+    constexpr int kh = t / 3, kw = t % 3;
+    if constexpr (DBG & 8) {
+      for (int j = 0; j < TN; ++j) F.bh[j] = F.bl[j] = (x6h8){};
+      for (int i = 0; i < TM; ++i) F.ah[i] = F.al[i] = (x6h8){};
+      return;
+    }
+    const char* abuf = lds + (c & 1) * ABYTES + kh * P * 128;
+    const char* bbuf = lds + B_OFF + slot * BSLOT;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int o = bad_[j] ^ (32 * s2);
+      F.bh[j] = *reinterpret_cast<const x6h8*>(bbuf + o);
+      F.bl[j] = *reinterpret_cast<const x6h8*>(bbuf + BIMG + o);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int o = aad[i][kw] ^ (32 * s2);
+      F.ah[i] = *reinterpret_cast<const x6h8*>(abuf + o);
+      F.al[i] = *reinterpret_cast<const x6h8*>(abuf + (o ^ 64));
+    }
+  };
+  auto mfma_frag = [&](const Frag& F) {
+    if constexpr (DBG & 1) {
+      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(F.ah[i]), "v"(F.al[i]));
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(F.bh[j]), "v"(F.bl[j]));
+      return;
+    }
+    // small terms first, the hi x hi term last (independent accumulators interleaved)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[i], F.bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+  };
+
+  // Barrier opening step (c, t): this wave's B(c, t) DMAs have landed (vmcnt = memory ops issued
+  // after them: B of the next D-1 steps, plus the halo loads if they were issued in the D steps
+  // before), every wave's have (barrier), and every wave finished reading step (c, t) - 1.
+  // Then: issue B(s + D); at t == TA the halo of chunk c + 1.
+  int slot = 0;  // ring slot of the current step
+  auto open_step = [&](int c, auto TAP, auto FIRST) {
+    constexpr int t = decltype(TAP)::value;
+    constexpr bool first = decltype(FIRST)::value;
+    constexpr int N = (D - 1) * BPS + (halo_in_window(t, D, TA, first) ? ALD : 0);
+    if constexpr (DBG & 16)
+      wait_vm<N>();
+    else
+      step_barrier<N>();
+    constexpr int tn = (t + D) % 9;
+    int ns = slot + D;
+    if (ns >= NSLOT) ns -= NSLOT;
+    b_issue(ns, tn, t + D >= 9 ? c + 1 : c);
+    if constexpr (t == TA) halo_issue(c + 1);
+  };
+
+  // ---- prologue: halo of chunk 0, B of steps 0 .. D-1, open step 0, its first fragments
+  halo_issue(0);
+#pragma unroll
+  for (int u = 0; u < D; ++u) b_issue(u % NSLOT, u, 0);
+  wait_vm<D * BPS>();
+  halo_tie();
+  halo_store(0);
+  open_step(0, std::integral_constant<int, 0>(), std::true_type());
+  load_frag(F0, 0, 0, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+
+  // step (c, t), software pipelined: [F1 reads] [MFMAs F0] [(t == 8) halo c+1 -> other buffer]
+  // [open step s+1] [F0 reads of s+1] [MFMAs F1]: every fragment read is in flight under the
+  // previous half-step's MFMAs, and the MFMAs after the barrier need no LDS wait.
+  auto step = [&](int c, auto TAP, auto FIRST) {
+    constexpr int t = decltype(TAP)::value;
+    constexpr bool first = decltype(FIRST)::value;
+    load_frag(F1, slot, c, TAP, std::integral_constant<int, 1>());
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs they overlap
+    mfma_frag(F0);
+    if constexpr (t == 8) {
+      // the halo of chunk c+1 was issued when step TA opened; younger: B issued at steps TA+1 .. 8
+      wait_vm<(8 - TA) * BPS>();
+      halo_tie();
+      halo_store((c + 1) & 1);
+    }
+    constexpr int t1 = (t + 1) % 9;
+    const int c1 = t == 8 ? c + 1 : c;
+    if (++slot == NSLOT) slot = 0;
+    open_step(c1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>());
+    load_frag(F0, slot, c1, std::integral_constant<int, t1>(), std::integral_constant<int, 0>());
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_frag(F1);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto chunk = [&](int c, auto FIRST) {
+    step(c, std::integral_constant<int, 0>(), FIRST);
+    step(c, std::integral_constant<int, 1>(), FIRST);
+    step(c, std::integral_constant<int, 2>(), FIRST);
+    step(c, std::integral_constant<int, 3>(), FIRST);
+    step(c, std::integral_constant<int, 4>(), FIRST);
+    step(c, std::integral_constant<int, 5>(), FIRST);
+    step(c, std::integral_constant<int, 6>(), FIRST);
+    step(c, std::integral_constant<int, 7>(), FIRST);
+    step(c, std::integral_constant<int, 8>(), FIRST);
+  };
+  chunk(0, std::true_type());
+  for (int c = 1; c < nchunks; ++c) chunk(c, std::false_type());
+  // drain the trailing (all-OOB) DMAs and LDS reads; every wave done with the ring and the halo
+  step_barrier<0>();
+
+  // ---- epilogue through LDS: the 256 x BN fp32 tile is parked as [pixel][BN], then every lane
+  // finishes 16-B channel quads: weight scale, alpha, bias, residual, ReLU, one 16-B store.
+  // C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  float* ct = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        ct[m * BN + (wn * TN + j) * 32 + li] = acc[i][j][r];
+      }
+  __syncthreads();
+  constexpr int QN = BN / 4;  // channel quads per pixel
+  bool bad = false;
+  const int qn = tid % QN;    // fixed per thread (NT % QN == 0)
+  static_assert(NT % QN == 0, "epilogue quads");
+  const int nq = n0 + 4 * qn;
+  const bool nv = nq < a.Cout;
+  x6f4 scl = {0.f, 0.f, 0.f, 0.f}, bia = {0.f, 0.f, 0.f, 0.f};
+  if (nv) {
+    scl = *reinterpret_cast<const x6f4*>(a.wsinv + nq) * a.alpha;
+    if (a.bias) bia = *reinterpret_cast<const x6f4*>(a.bias + nq);
+  }
+  float* out = a.out + (int64_t)nimg * a.out_sn + nq;
+  const float* res = a.res ? a.res + (int64_t)nimg * a.res_sn + nq : nullptr;
+  const int osh = (int)a.out_sh, osw = (int)a.out_sw;
+  const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
+  // every residual load in flight before the first use (latency-bound otherwise)
+  constexpr int IT = BM / (NT / QN);  // pixels per thread
+  x6f4 rv[IT];
+  int ooff[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int p = tid / QN + k * (NT / QN);
+    const int oy = oy0 + p / TW, ox = ox0 + p % TW;
+    const bool ok = nv && oy < a.Ho && ox < a.Wo;
+    ooff[k] = ok ? oy * osh + ox * osw : -1;
+    rv[k] = (res && ok) ? *reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw)) : (x6f4){0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    if (ooff[k] < 0) continue;
+    const int p = tid / QN + k * (NT / QN);
+    const x6f4 acc_v = *reinterpret_cast<const x6f4*>(ct + p * BN + 4 * qn);
+    bad |= !(__builtin_isfinite(acc_v.x) && __builtin_isfinite(acc_v.y) && __builtin_isfinite(acc_v.z) &&
+             __builtin_isfinite(acc_v.w));
+    x6f4 v = acc_v * scl + bia + rv[k];
+    if (a.relu) {
+      v.x = fmaxf(v.x, 0.f);
+      v.y = fmaxf(v.y, 0.f);
+      v.z = fmaxf(v.z, 0.f);
+      v.w = fmaxf(v.w, 0.f);
+    }
+    *reinterpret_cast<x6f4*>(out + ooff[k]) = v;
+  }
+  if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+}
+
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int DBG = 0>
+static void launch_x6_one(const ConvArgs& a, hipStream_t st) {
+  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
+  const int n_sp = a.Nimg * tiles_x * tiles_y;
+  const int ntn = (a.Cout + BN - 1) / BN;
+  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, DBG>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0, st,
+                     a, tiles_x, tiles_y, n_sp, ntn, a.Cin / 32);
+  DD_HIP_CHECK(hipGetLastError());
+}
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT>
+static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
+  static const int dbg = getenv("DDMI_X6_DBG") ? atoi(getenv("DDMI_X6_DBG")) : 0;
+  switch (dbg) {
+#define X6D(V) case V: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, V>(a, st); break;
+    X6D(0) X6D(1) X6D(2) X6D(4) X6D(6) X6D(8) X6D(16) X6D(14) X6D(15) X6D(9)
+#undef X6D
+    default: throw std::runtime_error("bad DDMI_X6_DBG");
+  }
+}
+
+// Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 conv this kernel covers (the
+// caller then takes conv_x5 / conv_x3).
+bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
+  if (a.prec != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || a.Cin % 32 != 0 || a.batch != 1 ||
+      a.b_kn)
+    return false;
+  if (a.Ho != a.H || a.Wo != a.W || a.Ho < 8) return false;
+  // the epilogue moves 16-B channel quads
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (a.Cout % 4 || a.out_sw % 4 || a.out_sh % 4 || a.out_sn % 4 || !al16(a.out) || !al16(a.wsinv) ||
+      (a.bias && !al16(a.bias)))
+    return false;
+  if (a.res && (a.res_sw % 4 || a.res_sh % 4 || a.res_sn % 4 || !al16(a.res))) return false;
+  // int32 offsets inside the kernel (the launcher checks the 2 GiB buffer-offset bound)
+  if ((int64_t)a.Nimg * a.in_sn >= (int64_t(1) << 29) || (int64_t)a.Cout * a.ldh >= (int64_t(1) << 30)) return false;
+  const bool wide = a.Ho < 16;  // 8 x 32 tiles for the 8-row maps (layer4 of the image trunk)
+  if (wide && a.Wo < 32) return false;
+  const int64_t n_sp = (int64_t)a.Nimg * (wide ? ((a.Ho + 7) / 8) * ((a.Wo + 31) / 32)
+                                               : ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16));
+  const bool bn128 = a.Cout > 64 && n_sp * ((a.Cout + 127) / 128) >= 256;
+  static const int cfg = getenv("DDMI_X6_CFG") ? atoi(getenv("DDMI_X6_CFG")) : 0;
+#define X6(TH, TW, BN, WM, WN, D, NS) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS>(a, st)
+  if (wide) {
+    if (bn128) {
+      X6(8, 32, 128, 4, 2, 3, 4);
+    } else {
+      if (cfg == 1) X6(8, 32, 64, 4, 2, 8, 9); else X6(8, 32, 64, 4, 2, 2, 3);
+    }
+  } else {
+    if (bn128) {
+      X6(16, 16, 128, 4, 2, 3, 4);
+    } else {
+      if (cfg == 1) X6(16, 16, 64, 4, 2, 8, 9); else X6(16, 16, 64, 4, 2, 2, 3);
+    }
+  }
+#undef X6
+  return true;
+}
+
+}  // namespace ddmi

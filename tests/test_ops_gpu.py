@@ -87,6 +87,12 @@ def test_conv2d(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     (16, 64, 64, 36, 200, 3, 1, 1, True, False),  # generic K path, ragged N in a 256-wide tile
     (1, 518, 518, 4, 64, 7, 2, 3, True, False),   # stem geometry (7x7/s2 on 4 padded channels)
     (3, 90, 250, 64, 256, 3, 2, 1, False, False), # stride 2, ragged M
+    # 3x3 / stride 1 convs take the halo-reuse direct kernel (conv_x6.hip)
+    (2, 8, 40, 128, 192, 3, 1, 1, True, True),    # 8 x 32 tiles, ragged W, BN 64 x 3
+    (1, 12, 70, 64, 100, 3, 1, 1, False, True),   # 8 x 32 tiles ragged in H and W, ragged N
+    (1, 20, 20, 96, 36, 3, 1, 1, True, False),    # 16 x 16 tiles ragged, Cout < BN
+    (8, 64, 64, 32, 200, 3, 1, 1, True, True),    # BN 128 ring (256 workgroups), ragged N
+    (64, 16, 16, 256, 256, 3, 1, 1, True, True),  # LiDAR layer3 shape
 ])
 def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     """f16x3 split-MFMA conv vs PyTorch-CPU fp32 (tolerance: fp32-class, 3e-5 of max|ref|)."""
@@ -125,6 +131,19 @@ def test_conv2d_f16x3_flags_overflow(gpu):
     xin, win = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1))
     ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), 1, 8, 8, 32, win.data_ptr(), None, None, out.data_ptr(), 32, 1, 1, 1, 0,
                            0, 0, flags.data_ptr(), None), gpu)
+    assert int(flags.item()) & 1
+
+
+def test_conv2d_x6_flags_overflow(gpu):
+    """The direct 3x3 kernel raises DD_NUM_F16_OVERFLOW_BIT too."""
+    x = rnd(1, 32, 16, 16, seed=15)
+    x[0, 5, 7, 9] = 1e6
+    w = rnd(64, 32, 3, 3, seed=16)
+    out = torch.empty(1, 16, 16, 64, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), 1, 16, 16, 32, win.data_ptr(), None, None, out.data_ptr(), 64, 3, 3, 1,
+                           1, 0, 0, flags.data_ptr(), None), gpu)
     assert int(flags.item()) & 1
 
 
