@@ -263,11 +263,14 @@ static void launch_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   DD_HIP_CHECK(hipGetLastError());
 }
 
+void set_last_conv_kernel(const char* k);  // conv_x3.hip
+
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st) {
   if (a.wh) {
     launch_conv_x3(a, st);
     return;
   }
+  set_last_conv_kernel("conv_gemm");
   if (a.Cin % 4 != 0) throw std::runtime_error("conv_gemm: Cin must be a multiple of 4");
   if ((a.in_sw % 4) || (a.in_sh % 4) || (a.in_sn % 4) || (reinterpret_cast<uintptr_t>(a.in) % 16))
     throw std::runtime_error("conv_gemm: input strides / base must be 16-byte aligned");

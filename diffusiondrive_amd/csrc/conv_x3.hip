@@ -532,6 +532,10 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st);  // conv_x5.hip
 bool launch_conv_x6(const ConvArgs& a, hipStream_t st);                 // conv_x6.hip
 
+static thread_local const char* g_last_conv = "conv_gemm";
+const char* last_conv_kernel() { return g_last_conv; }
+void set_last_conv_kernel(const char* k) { g_last_conv = k; }
+
 void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if (a.Cin % 4 != 0) throw std::runtime_error("conv_x3: Cin must be a multiple of 4");
   if ((a.in_sw % 4) || (a.in_sh % 4) || (a.in_sn % 4) || (reinterpret_cast<uintptr_t>(a.in) % 16))
@@ -555,10 +559,16 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   // default f16x3 path: 3x3 stride-1 convs on the halo-reuse direct kernel (conv_x6.hip), other
   // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
   static const int use_x6 = getenv("DDMI_X6") ? atoi(getenv("DDMI_X6")) : 1;
-  if (use_x6 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x6(a, st)) return;
-  static const int use_x5 = getenv("DDMI_X5") ? atoi(getenv("DDMI_X5")) : 1;
-  if (use_x5 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x5(a, M, K, st))
+  if (use_x6 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x6(a, st)) {
+    g_last_conv = "conv_x6";
     return;
+  }
+  static const int use_x5 = getenv("DDMI_X5") ? atoi(getenv("DDMI_X5")) : 1;
+  if (use_x5 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x5(a, M, K, st)) {
+    g_last_conv = "conv_x5";
+    return;
+  }
+  g_last_conv = "conv_x3";
   const int64_t t128 = ((M + 127) / 128) * (int64_t)((a.Cout + 127) / 128);
   const int64_t t256 = ((M + 255) / 256) * (int64_t)((a.Cout + 127) / 128);
   static const int big = getenv("DDMI_X3_BIG") ? atoi(getenv("DDMI_X3_BIG")) : 0;

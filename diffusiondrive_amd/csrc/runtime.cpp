@@ -372,6 +372,8 @@ class Model {
     DD_HIP_CHECK(hipEventRecord(a, st));
     f();
     DD_HIP_CHECK(hipEventRecord(b, st));
+    // conv / GEMM launches are attributed to the kernel the dispatcher actually chose
+    if (shape) name = last_conv_kernel();
     std::string detail;
     if (shape) {
       const ConvArgs& c = *shape;

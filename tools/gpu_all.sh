@@ -11,7 +11,7 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[$name] abnormal exit ($rc): stopping"; exit $rc; fi
   return $rc
 }
-step tests 900 python -m pytest tests -q -m gpu -x -rf || exit 1
+step tests 900 python -u -m pytest tests -q -m gpu -x -rf --timeout 300 --timeout-method thread || exit 1
 step bench 600 python bench.py ${BENCH_ARGS:-}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof" -o run -- python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1
