@@ -135,7 +135,7 @@ def main():
     conv_stats = {k: model.kernel_stats(k) for k in CONV_KERNELS}
     main_k = max(CONV_KERNELS, key=lambda k: conv_stats[k]["ms"])
     st = conv_stats[main_k]
-    other = {k: model.kernel_stats(k) for k in ("layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
+    other = {k: model.kernel_stats(k) for k in ("attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
                                                  "misc")}
     other.update({k: v for k, v in conv_stats.items() if k != main_k})
     model.set_profiling(False)
@@ -217,6 +217,8 @@ def main():
                                  "share_of_device_time": round(v["ms"] / total_prof_ms, 4) if total_prof_ms else None}
                              for k, v in conv_stats.items() if v["launches"]},
         },
+        "device_ms_per_step": {k: round(v["ms"] / prof_steps, 4) for k, v in
+                               sorted({main_k: st, **other}.items(), key=lambda kv: -kv[1]["ms"]) if v["launches"]},
         "whole_forward": {
             "gflop_per_scene": CANONICAL_GFLOP_PER_SCENE_2STEP if args.denoise_steps == 2 else None,
             "tflops": round(scenes_per_s / world * CANONICAL_GFLOP_PER_SCENE_2STEP / 1e3, 3)

@@ -89,6 +89,10 @@ void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, 
 void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldres, int res_div,
                       const float* g, const float* b, const float* film_scale, const float* film_shift,
                       float* y, int64_t ldy, int rows, int C, hipStream_t st);
+// Fused GPT self-attention (attention.hip): y[b,t,h*hs..] = softmax(q.k^T / sqrt(hs)) v per
+// (scene, head) from the packed projection qkv [B][T][3C]; y is [B][T][C]. T % 64 == 0, (T/4) % 8 == 0,
+// T <= 512, hs in {16, ..., 512}.
+void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, float* y, hipStream_t st);
 // Row softmax of (scale * x), in place, rows of length L (<= 1024), row stride ld.
 void launch_softmax_rows(float* x, int64_t ld, int rows, int L, float scale, hipStream_t st);
 // dst[r][:] = src[r % nsrc][:] for r < rows (row length C, contiguous).

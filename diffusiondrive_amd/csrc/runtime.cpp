@@ -553,7 +553,6 @@ class Model {
     float* X = buf("gpt_x", (size_t)B * T * C);
     float* Hb = buf("gpt_h", (size_t)B * T * C);
     float* QKV = buf("gpt_qkv", (size_t)B * T * 3 * C);
-    float* S = buf("gpt_s", (size_t)B * 4 * T * T);
     float* Y = buf("gpt_y", (size_t)B * T * C);
     float* MLP = buf("gpt_mlp", (size_t)B * T * 4 * C);
     float* LP = buf("gpt_lpool", (size_t)B * 64 * Cl);
@@ -569,52 +568,8 @@ class Model {
     for (const GptBlockW& w : g.blocks) {
       ln(w.ln1, X, C, Hb, C, M);
       gemm(w.qkv, Hb, C, M, QKV, 3 * C);
-      {  // S = Q K^T per (scene, head)
-        ConvArgs a;
-        a.in = QKV;
-        a.in_sn = 3 * C;
-        a.H = a.W = 1;
-        a.Cin = hs;
-        a.wgt = QKV + C;
-        a.ldb = 3 * C;
-        a.out = S;
-        a.out_sn = T;
-        a.Nimg = T;
-        a.Cout = T;
-        a.batch = B * 4;
-        a.zdiv = 4;
-        a.in_z1 = (int64_t)T * 3 * C;
-        a.in_z2 = hs;
-        a.w_z1 = (int64_t)T * 3 * C;
-        a.w_z2 = hs;
-        a.out_z1 = (int64_t)4 * T * T;
-        a.out_z2 = (int64_t)T * T;
-        launch("conv_gemm", 2.0 * B * 4 * T * T * hs, [&] { launch_conv_gemm(a, st); }, &a);
-      }
-      launch("softmax", 0, [&] { launch_softmax_rows(S, T, B * 4 * T, T, 1.0f / std::sqrt((float)hs), st); });
-      {  // Y = P V per (scene, head)
-        ConvArgs a;
-        a.in = S;
-        a.in_sn = T;
-        a.H = a.W = 1;
-        a.Cin = T;
-        a.wgt = QKV + 2 * C;
-        a.ldb = 3 * C;
-        a.b_kn = 1;
-        a.out = Y;
-        a.out_sn = C;
-        a.Nimg = T;
-        a.Cout = hs;
-        a.batch = B * 4;
-        a.zdiv = 4;
-        a.in_z1 = (int64_t)4 * T * T;
-        a.in_z2 = (int64_t)T * T;
-        a.w_z1 = (int64_t)T * 3 * C;
-        a.w_z2 = hs;
-        a.out_z1 = (int64_t)T * C;
-        a.out_z2 = hs;
-        launch("conv_gemm", 2.0 * B * 4 * T * T * hs, [&] { launch_conv_gemm(a, st); }, &a);
-      }
+      // softmax(Q K^T / sqrt(hs)) V per (scene, head), one fused fp32-MFMA launch (attention.hip)
+      launch("attn", 4.0 * B * T * T * (double)C, [&] { launch_gpt_attention(QKV, B, T, C, 4, Y, st); });
       gemm(w.proj, Y, C, M, X, C, false, X, C);  // x = x + proj(y)
       ln(w.ln2, X, C, Hb, C, M);
       gemm(w.mlp0, Hb, C, M, MLP, 4 * C, true);

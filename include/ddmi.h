@@ -169,6 +169,11 @@ int dd_op_bev_sample_attn(const float* logits, const float* pts, const float* va
                           int P, int Hv, int Wv, int C, void* stream);
 int dd_op_mha_small(const float* q, const float* k, const float* v, float* out, int B, int Lq, int Lk, int nh,
                     int hd, void* stream);
+/* Fused GPT self-attention core (replaces transfuser_backbone.py:386-410, SelfAttention.forward between
+ * the qkv projections and `proj`): qkv (B,T,3C) packed q | k | v, y (B,T,C) =
+ * softmax(q_h k_h^T / sqrt(C/heads)) v_h per (scene, head). T % 64 == 0 and (T/4) % 8 == 0 (T <= 512),
+ * C/heads in {16, 32, 64, 128, 256, 512}. */
+int dd_op_gpt_attention(const float* qkv, float* y, int B, int T, int C, int heads, void* stream);
 
 #ifdef __cplusplus
 }

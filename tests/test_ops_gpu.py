@@ -261,3 +261,18 @@ def test_mha_small(gpu, Lq, Lk):
     qd, kd, vd = g(q), g(k), g(v)
     ok(gpu.dd_op_mha_small(qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), B, Lq, Lk, nh, hd, None), gpu)
     close(out, ref, 1e-5)
+
+
+@pytest.mark.parametrize("B,T,C", [(2, 320, 64), (2, 320, 128), (1, 320, 256), (1, 320, 512), (1, 64, 1024),
+                                   (1, 320, 2048), (1, 128, 256)])
+def test_gpt_attention(gpu, B, T, C):
+    """Fused GPT self-attention (transfuser_backbone.py:386-410) vs the PyTorch fp32 restatement."""
+    nh, hs = 4, C // 4
+    qkv = rnd(B, T, 3 * C, seed=31)
+    q, k, v = (t.reshape(B, T, nh, hs).transpose(1, 2) for t in qkv.split(C, -1))
+    att = torch.softmax((q @ k.transpose(-2, -1)) * (1.0 / np.sqrt(hs)), -1)
+    ref = (att @ v).transpose(1, 2).reshape(B, T, C)
+    out = torch.empty(B, T, C, device=DEV)
+    qd = g(qkv)
+    ok(gpu.dd_op_gpt_attention(qd.data_ptr(), out.data_ptr(), B, T, C, nh, None), gpu)
+    close(out, ref, 2e-5)

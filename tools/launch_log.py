@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 PEAK = 157.3
+PEAK_X3 = 2500.0 / 3
 
 
 def main():
@@ -57,7 +58,7 @@ def main():
             name, detail, flops, ms = line.rstrip("\n").split("\t")
             ms = float(ms) / a.reps
             total += ms
-            if name not in ("conv_gemm", "conv_x3"):
+            if not detail:
                 other[name] += ms
                 continue
             g = groups.setdefault(f"{name} {detail}", [0, 0.0, 0.0])
@@ -65,18 +66,25 @@ def main():
             g[1] += float(flops) / a.reps
             g[2] += ms
     rows = sorted(groups.items(), key=lambda kv: -kv[1][2])
-    lines = [f"# conv_gemm launches per forward (B={a.batch}, {a.arch}, gemm={a.gemm}); forward device total {total:.2f} ms", "",
-             "| shape | launches | ms | GFLOP | TFLOP/s | frac fp32 peak | share |", "|---|---|---|---|---|---|---|"]
+    lines = [f"# conv / GEMM launches per forward (B={a.batch}, {a.arch}, gemm={a.gemm}); forward device total {total:.2f} ms", "",
+             "| kernel / shape | launches | ms | GFLOP | TFLOP/s | frac fp32 peak | frac f16x3 ceiling | share |", "|---|---|---|---|---|---|---|---|"]
     cg_ms = sum(v[2] for _, v in rows)
     cg_fl = sum(v[1] for _, v in rows)
     for d, (n, fl, ms) in rows:
         n //= a.reps
         tf = fl / (ms * 1e-3) / 1e12 if ms else 0
-        lines.append(f"| {d} | {n} | {ms:.3f} | {fl / 1e9:.1f} | {tf:.1f} | {tf / PEAK:.3f} | {ms / total:.3f} |")
-    lines.append(f"| **GEMM total (conv_gemm + conv_x3)** | | {cg_ms:.3f} | {cg_fl / 1e9:.1f} | {cg_fl / cg_ms / 1e9:.1f} | "
-                 f"{cg_fl / cg_ms / 1e9 / PEAK:.3f} | {cg_ms / total:.3f} |")
+        lines.append(f"| {d} | {n} | {ms:.3f} | {fl / 1e9:.1f} | {tf:.1f} | {tf / PEAK:.3f} | {tf / PEAK_X3:.3f} | "
+                     f"{ms / total:.3f} |")
+    lines.append(f"| **GEMM / conv total** | | {cg_ms:.3f} | {cg_fl / 1e9:.1f} | {cg_fl / cg_ms / 1e9:.1f} | "
+                 f"{cg_fl / cg_ms / 1e9 / PEAK:.3f} | {cg_fl / cg_ms / 1e9 / PEAK_X3:.3f} | {cg_ms / total:.3f} |")
+    by_k = collections.defaultdict(lambda: [0.0, 0.0])
+    for d, (n, fl, ms) in rows:
+        by_k[d.split()[0]][0] += ms
+        by_k[d.split()[0]][1] += fl
+    for k, (ms, fl) in sorted(by_k.items(), key=lambda kv: -kv[1][0]):
+        lines.append(f"| {k} (all shapes) | | {ms:.3f} | {fl / 1e9:.1f} | {fl / ms / 1e9:.1f} | | | {ms / total:.3f} |")
     for k, v in sorted(other.items(), key=lambda kv: -kv[1]):
-        lines.append(f"| {k} | | {v:.3f} | | | | {v / total:.3f} |")
+        lines.append(f"| {k} | | {v:.3f} | | | | | {v / total:.3f} |")
     txt = "\n".join(lines) + "\n"
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:

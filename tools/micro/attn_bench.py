@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Microbenchmark of the fused GPT attention op (dd_op_gpt_attention) at the bench shapes (B=64, T=320)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from diffusiondrive_amd import _lib  # noqa: E402
+
+lib = _lib.load()
+B, T = 64, 320
+for C in (64, 128, 256, 512):
+    qkv = torch.randn(B, T, 3 * C, device="cuda")
+    y = torch.empty(B, T, C, device="cuda")
+    for _ in range(3):
+        _lib.check(lib.dd_op_gpt_attention(qkv.data_ptr(), y.data_ptr(), B, T, C, 4, None), lib, op=True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 20
+    e0.record()
+    for _ in range(n):
+        lib.dd_op_gpt_attention(qkv.data_ptr(), y.data_ptr(), B, T, C, 4, None)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    fl = 4.0 * B * T * T * C
+    print(f"C={C:4d} hs={C // 4:3d}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
