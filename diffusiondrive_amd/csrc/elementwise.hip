@@ -253,11 +253,98 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
+// Vectorised variant for power-of-two C >= 64 with 16-B aligned rows: a row is spread over LPR lanes
+// (min(64, C/4)), each holding VPL float4 channel quads, so a wave normalises 64/LPR rows at once
+// with 16-B loads / stores and a log2(LPR)-step reduction. Same two-pass arithmetic as above.
+template <int LPR, int VPL>
+__global__ __launch_bounds__(256) void layernorm_v4_kernel(const float* __restrict__ x, int64_t ldx,
+                                                           const float* __restrict__ res, int64_t ldres, int res_div,
+                                                           const float* __restrict__ g, const float* __restrict__ b,
+                                                           const float* __restrict__ fs, const float* __restrict__ fb,
+                                                           float* y, int64_t ldy, int rows) {
+  constexpr int C = LPR * 4 * VPL;
+  const int sub = threadIdx.x % LPR;
+  const int row = (blockIdx.x * 256 + threadIdx.x) / LPR;
+  const bool live = row < rows;
+  const int r = live ? row : rows - 1;  // dead lanes still join the xor reductions
+  const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)r * ldx);
+  const float4* rr = res ? reinterpret_cast<const float4*>(res + (int64_t)(r / res_div) * ldres) : nullptr;
+  float4 v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    float4 t = xr[sub + LPR * i];
+    if (rr) {
+      const float4 u = rr[sub + LPR * i];
+      t.x += u.x;
+      t.y += u.y;
+      t.z += u.z;
+      t.w += u.w;
+    }
+    v[i] = t;
+    s += (t.x + t.y) + (t.z + t.w);
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+    q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q / (float)C + 1e-5f);
+  if (!live) return;
+  float4* yr = reinterpret_cast<float4*>(y + (int64_t)row * ldy);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c4 = sub + LPR * i;
+    const float4 gg = reinterpret_cast<const float4*>(g)[c4], bb = reinterpret_cast<const float4*>(b)[c4];
+    float4 o;
+    o.x = (v[i].x - mean) * rstd * gg.x + bb.x;
+    o.y = (v[i].y - mean) * rstd * gg.y + bb.y;
+    o.z = (v[i].z - mean) * rstd * gg.z + bb.z;
+    o.w = (v[i].w - mean) * rstd * gg.w + bb.w;
+    if (fs) {
+      const float4 a = reinterpret_cast<const float4*>(fs)[c4], c = reinterpret_cast<const float4*>(fb)[c4];
+      o.x = o.x * (1.f + a.x) + c.x;
+      o.y = o.y * (1.f + a.y) + c.y;
+      o.z = o.z * (1.f + a.z) + c.z;
+      o.w = o.w * (1.f + a.w) + c.w;
+    }
+    yr[c4] = o;
+  }
+}
+
 void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldres, int res_div, const float* g,
                       const float* b, const float* film_scale, const float* film_shift, float* y, int64_t ldy,
                       int rows, int C, hipStream_t st) {
   if (C > 2048) throw std::runtime_error("layernorm: C > 2048");
   if (rows == 0) return;
+  auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool vec = C >= 64 && (C & (C - 1)) == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (!res || ldres % 4 == 0) &&
+                   al(x) && al(y) && al(res) && al(g) && al(b) && al(film_scale) && al(film_shift);
+  if (vec) {
+    const int lpr = C / 4 < 64 ? C / 4 : 64;
+    const dim3 grid((unsigned)(((int64_t)rows * lpr + 255) / 256));
+    const int rd = res_div < 1 ? 1 : res_div;
+#define LNV(L, V)                                                                                                  \
+  hipLaunchKernelGGL((layernorm_v4_kernel<L, V>), grid, dim3(256), 0, st, x, ldx, res, ldres, rd, g, b, film_scale, \
+                     film_shift, y, ldy, rows)
+    switch (C) {
+      case 64: LNV(16, 1); break;
+      case 128: LNV(32, 1); break;
+      case 256: LNV(64, 1); break;
+      case 512: LNV(64, 2); break;
+      case 1024: LNV(64, 4); break;
+      default: LNV(64, 8); break;
+    }
+#undef LNV
+    DD_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, ldx, res, ldres,
                      res_div < 1 ? 1 : res_div, g, b, film_scale, film_shift, y, ldy, rows, C);
   DD_HIP_CHECK(hipGetLastError());

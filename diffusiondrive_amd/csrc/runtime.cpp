@@ -117,8 +117,13 @@ class Model {
   std::vector<PendingEv> pending;
   std::vector<hipEvent_t> ev_pool;
   std::map<std::string, KStat> stats;
-  hipStream_t st = nullptr;   // the handle's own non-blocking stream (capturable)
+  hipStream_t st = nullptr;   // the stream launches go to (the handle's main stream, or a side stream)
+  hipStream_t st_main = nullptr, st_side = nullptr;  // the handle's own non-blocking streams (capturable)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  // fork / join events of one forward (reused across forwards: every record precedes its wait)
+  std::vector<hipEvent_t> fj_ev;
+  size_t fj_next = 0;
+  bool use_side = true;  // DDMI_STREAMS=0: everything on the main stream
   // graph cache keyed by the forward's shape signature and the buffer generation
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
@@ -134,7 +139,10 @@ class Model {
     build(bx);
     ar.upload();
     decoder_init_constants();
-    DD_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_main, hipStreamNonBlocking));
+    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_side, hipStreamNonBlocking));
+    st = st_main;
+    if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -167,11 +175,14 @@ class Model {
   }
 
   ~Model() {
-    if (st) (void)hipStreamSynchronize(st);
+    if (st_main) (void)hipStreamSynchronize(st_main);
+    if (st_side) (void)hipStreamSynchronize(st_side);
     if (graph.exec) (void)hipGraphExecDestroy(graph.exec);
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
-    if (st) (void)hipStreamDestroy(st);
+    for (auto& e : fj_ev) (void)hipEventDestroy(e);
+    if (st_main) (void)hipStreamDestroy(st_main);
+    if (st_side) (void)hipStreamDestroy(st_side);
     if (num_flags) (void)hipFree(num_flags);
     for (auto& kv : bufs) (void)hipFree(kv.second.first);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
@@ -351,6 +362,45 @@ class Model {
     bufs[name] = {p, n};
     ++generation;
     return p;
+  }
+
+  // ---- two-stream fork / join. Independent branches of the forward (the LiDAR trunk stage beside
+  // the image one, the tf decoder beside the FPN / bev_proj / value_proj chain, the optional heads
+  // beside the trajectory head) are issued on the side stream between fork() and join(); under
+  // stream capture this becomes a graph with parallel branches, so a branch's small launches fill
+  // CUs the other leaves idle. side(f) runs f with every launch going to the side stream.
+  hipEvent_t fj_event() {
+    if (fj_next == fj_ev.size()) {
+      hipEvent_t e;
+      DD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      fj_ev.push_back(e);
+    }
+    return fj_ev[fj_next++];
+  }
+  // profiled runs stay on one stream: per-launch event timing needs launches that do not overlap
+  bool sides() const { return use_side && !profiling; }
+  void fork() {
+    if (!sides()) return;
+    hipEvent_t e = fj_event();
+    DD_HIP_CHECK(hipEventRecord(e, st_main));
+    DD_HIP_CHECK(hipStreamWaitEvent(st_side, e, 0));
+  }
+  void join() {
+    if (!sides()) return;
+    hipEvent_t e = fj_event();
+    DD_HIP_CHECK(hipEventRecord(e, st_side));
+    DD_HIP_CHECK(hipStreamWaitEvent(st_main, e, 0));
+  }
+  template <class F>
+  void side(F&& f) {
+    st = sides() ? st_side : st_main;
+    try {
+      f();
+    } catch (...) {
+      st = st_main;
+      throw;
+    }
+    st = st_main;
   }
 
   template <class F>
@@ -604,31 +654,78 @@ class Model {
     const float* stat = bufs["in_status"].first;
     const float* noise = bufs["in_noise"].first;
 
-    // ---- stems + maxpool (timm conv1/bn1/act1/maxpool)
+    // ---- stems + maxpool (timm conv1/bn1/act1/maxpool); the LiDAR trunk runs on the side stream
+    fj_next = 0;
     int hi = (HC + 6 - 7) / 2 + 1, wi = (WC + 6 - 7) / 2 + 1;
     float* stem_i = buf("img_stem", (size_t)B * hi * wi * 64);
-    conv_c(img.stem, cam4, B, HC, WC, stem_i, true);
     int hl = (HL + 6 - 7) / 2 + 1, wl = (WL + 6 - 7) / 2 + 1;
     float* stem_l = buf("lid_stem", (size_t)B * hl * wl * 64);
-    conv_c(lid.stem, lid4, B, HL, WL, stem_l, true);
     const int hi2 = (hi + 2 - 3) / 2 + 1, wi2 = (wi + 2 - 3) / 2 + 1;
     float* pool_i = buf("img_pool", (size_t)B * hi2 * wi2 * 64);
-    launch("pool", 0, [&] { launch_maxpool3x3s2(stem_i, pool_i, B, hi, wi, 64, hi2, wi2, st); });
     const int hl2 = (hl + 2 - 3) / 2 + 1, wl2 = (wl + 2 - 3) / 2 + 1;
     float* pool_l = buf("lid_pool", (size_t)B * hl2 * wl2 * 64);
-    launch("pool", 0, [&] { launch_maxpool3x3s2(stem_l, pool_l, B, hl, wl, 64, hl2, wl2, st); });
+    fork();
+    side([&] {
+      conv_c(lid.stem, lid4, B, HL, WL, stem_l, true);
+      launch("pool", 0, [&] { launch_maxpool3x3s2(stem_l, pool_l, B, hl, wl, 64, hl2, wl2, st); });
+    });
+    conv_c(img.stem, cam4, B, HC, WC, stem_i, true);
+    launch("pool", 0, [&] { launch_maxpool3x3s2(stem_i, pool_i, B, hi, wi, 64, hi2, wi2, st); });
 
-    // ---- 4 scales: trunk stages + GPT fusion
+    // ---- 4 scales: trunk stages (image on the main stream, LiDAR beside it) + GPT fusion
     float* xi = pool_i;
     float* xl = pool_l;
     int Hi = hi2, Wi = wi2, Hl = hl2, Wl = wl2;
     for (int s = 0; s < 4; ++s) {
+      if (s > 0) fork();
+      side([&] { xl = run_stage(lid, s, xl, B, Hl, Wl, "lid"); });
       xi = run_stage(img, s, xi, B, Hi, Wi, "img");
-      xl = run_stage(lid, s, xl, B, Hl, Wl, "lid");
+      join();
       fuse(s, xi, B, Hi, Wi, xl, Hl, Wl);
     }
     alias("img_l4", xi);
     alias("bev_feature", xl);  // (B, 8, 8, 512) NHWC; transformer_decoder_join -> fused = lidar (:204-205)
+
+    // ---- BEV tokens + status -> keyval (B, 65, 256) (+= _keyval_embedding)
+    float* KV = buf("keyval", (size_t)B * 65 * d);
+    conv(bev_down, xl, (int64_t)Hl * Wl * 512, (int64_t)Wl * 512, 512, B, Hl, Wl, KV, (int64_t)65 * d, (int64_t)Wl * d,
+         d, false, W(kv_emb), 0, (int64_t)Wl * d, d);
+    gemm_g(status, stat, 8, 8, B, 1, KV + (size_t)64 * d, (int64_t)65 * d, d, false, W(kv_emb) + (size_t)64 * d, 0, d);
+
+    // ---- _tf_decoder: 3 post-norm layers over 31 queries, memory = keyval (:141-142), on the side
+    // stream beside the FPN / bev_proj / value_proj chain below
+    const int NQ = 31;
+    float* q = buf("query_out", (size_t)B * NQ * d);
+    fork();
+    side([&] {
+      launch("misc", 0, [&] { launch_broadcast_rows(W(q_emb), NQ, q, B * NQ, d, st); });
+      float* qkv = buf("tf_qkv", (size_t)B * NQ * 3 * d);
+      float* att = buf("tf_att", (size_t)B * NQ * d);
+      float* tmp = buf("tf_tmp", (size_t)B * NQ * d);
+      float* kvp = buf("tf_kvp", (size_t)B * 65 * 2 * d);
+      float* ff = buf("tf_ff", (size_t)B * NQ * 1024);
+      const int MQ = B * NQ;
+      for (const TfLayerW& w : tf) {
+        gemm(w.sa_in, q, d, MQ, qkv, 3 * d);
+        launch("mha", 0, [&] {
+          launch_mha_small(qkv, 3 * d, qkv + d, qkv + 2 * d, 3 * d, att, d, B, NQ, NQ, 8, 32, (int64_t)NQ * 3 * d,
+                           (int64_t)NQ * 3 * d, (int64_t)NQ * d, st);
+        });
+        gemm(w.sa_out, att, d, MQ, tmp, d, false, q, d);
+        ln(w.n1, tmp, d, q, d, MQ);
+        gemm(w.ca_q, q, d, MQ, qkv, d);
+        gemm(w.ca_kv, KV, d, B * 65, kvp, 2 * d);
+        launch("mha", 0, [&] {
+          launch_mha_small(qkv, d, kvp, kvp + d, 2 * d, att, d, B, NQ, 65, 8, 32, (int64_t)NQ * d, (int64_t)65 * 2 * d,
+                           (int64_t)NQ * d, st);
+        });
+        gemm(w.ca_out, att, d, MQ, tmp, d, false, q, d);
+        ln(w.n2, tmp, d, q, d, MQ);
+        gemm(w.l1, q, d, MQ, ff, 1024, true);
+        gemm(w.l2, ff, 1024, MQ, tmp, d, false, q, d);
+        ln(w.n3, tmp, d, q, d, MQ);
+      }
+    });
 
     // ---- FPN top_down (transfuser_backbone.py:153-159); p3 lands in channels 256..319 of the
     // concat buffer that feeds bev_proj (transfuser_model_v2.py:123-140).
@@ -656,11 +753,6 @@ class Model {
     conv(up4, up3, (int64_t)HB * WB * bc, (int64_t)WB * bc, bc, B, HB, WB, cross_in + 256, (int64_t)HB * WB * CC,
          (int64_t)WB * CC, CC, true);
 
-    // ---- BEV tokens + status -> keyval (B, 65, 256) (+= _keyval_embedding)
-    float* KV = buf("keyval", (size_t)B * 65 * d);
-    conv(bev_down, xl, (int64_t)Hl * Wl * 512, (int64_t)Wl * 512, 512, B, Hl, Wl, KV, (int64_t)65 * d, (int64_t)Wl * d,
-         d, false, W(kv_emb), 0, (int64_t)Wl * d, d);
-    gemm_g(status, stat, 8, 8, B, 1, KV + (size_t)64 * d, (int64_t)65 * d, d, false, W(kv_emb) + (size_t)64 * d, 0, d);
     // concat_cross_bev: keyval[:, :64] as (B,8,8,256) -> bilinear 64x64 -> channels 0..255
     {
       View4 a{KV, (int64_t)65 * d, (int64_t)8 * d, d, 1};
@@ -672,72 +764,49 @@ class Model {
     gemm(bevproj, cross_in, CC, MB, cross, d, true);
     ln(bevproj_ln, cross, d, cross, d, MB);
 
-    // ---- _tf_decoder: 3 post-norm layers over 31 queries, memory = keyval (:141-142)
-    const int NQ = 31;
-    float* q = buf("query_out", (size_t)B * NQ * d);
-    launch("misc", 0, [&] { launch_broadcast_rows(W(q_emb), NQ, q, B * NQ, d, st); });
-    float* qkv = buf("tf_qkv", (size_t)B * NQ * 3 * d);
-    float* att = buf("tf_att", (size_t)B * NQ * d);
-    float* tmp = buf("tf_tmp", (size_t)B * NQ * d);
-    float* kvp = buf("tf_kvp", (size_t)B * 65 * 2 * d);
-    float* ff = buf("tf_ff", (size_t)B * NQ * 1024);
-    const int MQ = B * NQ;
-    for (const TfLayerW& w : tf) {
-      gemm(w.sa_in, q, d, MQ, qkv, 3 * d);
-      launch("mha", 0, [&] {
-        launch_mha_small(qkv, 3 * d, qkv + d, qkv + 2 * d, 3 * d, att, d, B, NQ, NQ, 8, 32, (int64_t)NQ * 3 * d,
-                         (int64_t)NQ * 3 * d, (int64_t)NQ * d, st);
-      });
-      gemm(w.sa_out, att, d, MQ, tmp, d, false, q, d);
-      ln(w.n1, tmp, d, q, d, MQ);
-      gemm(w.ca_q, q, d, MQ, qkv, d);
-      gemm(w.ca_kv, KV, d, B * 65, kvp, 2 * d);
-      launch("mha", 0, [&] {
-        launch_mha_small(qkv, d, kvp, kvp + d, 2 * d, att, d, B, NQ, 65, 8, 32, (int64_t)NQ * d, (int64_t)65 * 2 * d,
-                         (int64_t)NQ * d, st);
-      });
-      gemm(w.ca_out, att, d, MQ, tmp, d, false, q, d);
-      ln(w.n2, tmp, d, q, d, MQ);
-      gemm(w.l1, q, d, MQ, ff, 1024, true);
-      gemm(w.l2, ff, 1024, MQ, tmp, d, false, q, d);
-      ln(w.n3, tmp, d, q, d, MQ);
+    // value_proj for both decoder layers (main stream, beside the tf decoder), then join
+    const int R = B * Q;  // trajectory query rows
+    float* vals[2];
+    for (int l = 0; l < 2; ++l) {
+      vals[l] = buf("value_l" + std::to_string(l), (size_t)MB * d);
+      conv_c(dl[l].vproj, cross, B, HB, WB, vals[l], true);
     }
+    join();
     const float* ego = q;          // row 0 of each scene
     const float* agents = q + d;   // rows 1..30
 
-    // ---- optional heads (off the waypoint path)
-    if (heads) {
-      float* s1 = buf("sem_h", (size_t)B * HB * WB * bc);
-      conv(sem0, cross_in + 256, (int64_t)HB * WB * CC, (int64_t)WB * CC, CC, B, HB, WB, s1, (int64_t)HB * WB * bc,
-           (int64_t)WB * bc, bc, true);
-      float* s2 = buf("sem_logits", (size_t)B * HB * WB * 8);
-      conv(sem2, s1, (int64_t)HB * WB * bc, (int64_t)WB * bc, bc, B, HB, WB, s2, (int64_t)HB * WB * 7, (int64_t)WB * 7, 7,
-           false);
-      const int SH = HL / 2, SW = WL;
-      float* sem = buf("bev_semantic_map", (size_t)B * 7 * SH * SW);
-      View4 a{s2, (int64_t)HB * WB * 7, (int64_t)WB * 7, 7, 1};
-      View4 o{sem, (int64_t)7 * SH * SW, SW, 1, (int64_t)SH * SW};
-      launch("bilinear", 0, [&] {
-        launch_bilinear(a, B, HB, WB, 7, o, SH, SW, (float)HB / SH, (float)WB / SW, 0, st);
-      });
-      float* a1 = buf("agent_h", (size_t)B * 30 * 1024);
-      gemm_g(ag0, agents, (int64_t)NQ * d, d, B, 30, a1, (int64_t)30 * 1024, 1024, true);
-      float* ast = buf("agent_states", (size_t)B * 30 * 5);
-      gemm(ag2, a1, 1024, B * 30, ast, 5);
-      launch("misc", 0, [&] { launch_agent_post(ast, B * 30, st); });
-      float* alb = buf("agent_labels", (size_t)B * 30);
-      gemm_g(agl, agents, (int64_t)NQ * d, d, B, 30, alb, 30, 1);
-    }
+    // ---- optional heads (off the waypoint path), on the side stream beside the trajectory head
+    fork();
+    side([&] {
+      if (heads) {
+        float* s1 = buf("sem_h", (size_t)B * HB * WB * bc);
+        conv(sem0, cross_in + 256, (int64_t)HB * WB * CC, (int64_t)WB * CC, CC, B, HB, WB, s1, (int64_t)HB * WB * bc,
+             (int64_t)WB * bc, bc, true);
+        float* s2 = buf("sem_logits", (size_t)B * HB * WB * 8);
+        conv(sem2, s1, (int64_t)HB * WB * bc, (int64_t)WB * bc, bc, B, HB, WB, s2, (int64_t)HB * WB * 7, (int64_t)WB * 7, 7,
+             false);
+        const int SH = HL / 2, SW = WL;
+        float* sem = buf("bev_semantic_map", (size_t)B * 7 * SH * SW);
+        View4 a{s2, (int64_t)HB * WB * 7, (int64_t)WB * 7, 7, 1};
+        View4 o{sem, (int64_t)7 * SH * SW, SW, 1, (int64_t)SH * SW};
+        launch("bilinear", 0, [&] {
+          launch_bilinear(a, B, HB, WB, 7, o, SH, SW, (float)HB / SH, (float)WB / SW, 0, st);
+        });
+        float* a1 = buf("agent_h", (size_t)B * 30 * 1024);
+        gemm_g(ag0, agents, (int64_t)NQ * d, d, B, 30, a1, (int64_t)30 * 1024, 1024, true);
+        float* ast = buf("agent_states", (size_t)B * 30 * 5);
+        gemm(ag2, a1, 1024, B * 30, ast, 5);
+        launch("misc", 0, [&] { launch_agent_post(ast, B * 30, st); });
+        float* alb = buf("agent_labels", (size_t)B * 30);
+        gemm_g(agl, agents, (int64_t)NQ * d, d, B, 30, alb, 30, 1);
+      }
+    });
 
     // ---- trajectory head (TrajectoryHead.forward_test, :578-641)
-    const int R = B * Q;  // trajectory query rows
-    float* vals[2];
     float* egos[2];
     float* akv[2];
     for (int l = 0; l < 2; ++l) {
       const DiffLayerW& w = dl[l];
-      vals[l] = buf("value_l" + std::to_string(l), (size_t)MB * d);
-      conv_c(w.vproj, cross, B, HB, WB, vals[l], true);
       float* e1 = buf("ego_v" + std::to_string(l), (size_t)B * d);
       gemm_g(w.eg_v, ego, (int64_t)NQ * d, d, B, 1, e1, d, d);
       egos[l] = buf("ego_out" + std::to_string(l), (size_t)B * d);
@@ -849,6 +918,7 @@ class Model {
     float* traj = buf("trajectory", (size_t)B * P * 3);
     int* idx = reinterpret_cast<int*>(buf("mode_idx", B));
     launch("misc", 0, [&] { launch_select_mode(cls_last, reg_last, traj, idx, B, Q, P, st); });
+    join();  // the heads branch
     alias("poses_reg", reg_last);
     alias("poses_cls", cls_last);
   }

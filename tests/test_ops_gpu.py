@@ -177,7 +177,8 @@ def test_gemm_batched(gpu, batch, M, N, K, kn):
 
 
 @pytest.mark.parametrize("rows,C,res_div,film", [(1000, 256, 0, False), (333, 64, 20, True), (50, 2048, 0, False),
-                                                 (20, 1024, 4, False)])
+                                                 (20, 1024, 4, False), (77, 128, 0, True), (129, 512, 3, False),
+                                                 (45, 320, 0, False)])
 def test_layernorm(gpu, rows, C, res_div, film):
     x = rnd(rows, C, seed=11, scale=3.0) + 0.5
     gam, bet = rnd(C, seed=12), rnd(C, seed=13)
