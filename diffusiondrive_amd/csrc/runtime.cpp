@@ -834,7 +834,6 @@ class Model {
     float* logit = buf("bev_logits", (size_t)R * 8);
     float* gs = buf("gs", (size_t)R * d);
     float* x1 = buf("dx1", (size_t)R * d);
-    float* x2 = buf("dx2", (size_t)R * d);
     float* x3 = buf("dx3", (size_t)R * d);
     float* qa = buf("dqa", (size_t)R * d);
     float* hf = buf("dffn", (size_t)R * 1024);
@@ -855,22 +854,32 @@ class Model {
     float* cls_last = nullptr;
     for (int si = 0; si < steps; ++si) {
       const int k = roll[si];
+      // time embedding -> Mish -> FiLM scale / shift of both layers, on the side stream beside the
+      // trajectory embedding and the first layer's attention / FFN (joined before its norm3)
+      float* mte = buf("temb_mish", d);
+      float* film_ss[2];
+      for (int l = 0; l < 2; ++l)
+        film_ss[l] = buf("film_s" + std::to_string(si) + "l" + std::to_string(l), 2 * d);
+      fork();
+      side([&] {
+        launch("misc", 0, [&] { launch_timestep_embed((float)k, te0, d, st); });
+        gemm(tm1, te0, d, 1, te1, 4 * d);
+        launch("misc", 0, [&] { launch_activation(te1, te1, 4 * d, 0, st); });
+        gemm(tm3, te1, 4 * d, 1, te2, d);
+        launch("misc", 0, [&] { launch_activation(te2, mte, d, 0, st); });
+        for (int l = 0; l < 2; ++l) gemm(dl[l].film, mte, d, 1, film_ss[l], 2 * d);
+      });
       launch("misc", 0, [&] { launch_traj_embed(imgx, pts, emb, R, P, st); });
       gemm(pa0, emb, 512, R, tf1, d, true);
       ln(pa2, tf1, d, tf1, d, R);
       gemm(pa3, tf1, d, R, tfe, d);
-      launch("misc", 0, [&] { launch_timestep_embed((float)k, te0, d, st); });
-      gemm(tm1, te0, d, 1, te1, 4 * d);
-      launch("misc", 0, [&] { launch_activation(te1, te1, 4 * d, 0, st); });
-      gemm(tm3, te1, 4 * d, 1, te2, d);
-      float* mte = buf("temb_mish", d);
-      launch("misc", 0, [&] { launch_activation(te2, mte, d, 0, st); });
       const float* cur = pts;
       for (int l = 0; l < 2; ++l) {
         const DiffLayerW& w = dl[l];
         const std::string sfx = "_s" + std::to_string(si) + "l" + std::to_string(l);
-        float* ss = buf("film" + sfx, 2 * d);
-        gemm(w.film, mte, d, 1, ss, 2 * d);
+        float* ss = film_ss[l];
+        // per-(step, layer) buffer: the cls branch of this layer reads it beside the next layer
+        float* x2 = buf("dx2" + sfx, (size_t)R * d);
         // GridSampleCrossBEVAttention
         gemm(w.attw, tfe, d, R, logit, P);
         float* gso = buf("gs" + sfx, (size_t)R * d);
@@ -891,14 +900,18 @@ class Model {
         // ffn -> norm3 -> FiLM time modulation
         gemm(w.ffn0, x3, d, R, hf, 1024, true);
         gemm(w.ffn2, hf, 1024, R, x2, d);
+        if (l == 0) join();  // FiLM scale / shift from the side stream
         ln(w.n3, x2, d, x2, d, R, nullptr, 0, 1, ss, ss + d);
-        // task decoder
-        gemm(w.c0, x2, d, R, c1, d, true);
-        ln(w.c2, c1, d, c1, d, R);
-        gemm(w.c3, c1, d, R, c2, d, true);
-        ln(w.c5, c2, d, c2, d, R);
+        // task decoder: cls branch on the side stream beside the reg branch (and the next layer)
         float* cls = buf("cls" + sfx, R);
-        gemm(w.c6, c2, d, R, cls, 1);
+        fork();
+        side([&] {
+          gemm(w.c0, x2, d, R, c1, d, true);
+          ln(w.c2, c1, d, c1, d, R);
+          gemm(w.c3, c1, d, R, c2, d, true);
+          ln(w.c5, c2, d, c2, d, R);
+          gemm(w.c6, c2, d, R, cls, 1);
+        });
         gemm(w.r0, x2, d, R, r1, d, true);
         gemm(w.r2, r1, d, R, r2, d, true);
         gemm(w.r4, r2, d, R, rr, P * 3);
@@ -917,8 +930,8 @@ class Model {
     }
     float* traj = buf("trajectory", (size_t)B * P * 3);
     int* idx = reinterpret_cast<int*>(buf("mode_idx", B));
+    join();  // the cls branches (and the heads branch before them on the side stream)
     launch("misc", 0, [&] { launch_select_mode(cls_last, reg_last, traj, idx, B, Q, P, st); });
-    join();  // the heads branch
     alias("poses_reg", reg_last);
     alias("poses_cls", cls_last);
   }
