@@ -40,8 +40,9 @@ KERNEL_DESC = {
     "conv_x3": "conv_x3 (implicit-GEMM conv / GEMM, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
     "conv_x5": "conv_x5 (implicit-GEMM conv, LDS-DMA staging, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
     "conv_x6": "conv_x6 (halo-reuse direct 3x3 conv, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
+    "gemm_lat": "gemm_lat (whole-K small GEMM, fp32 MFMA v_mfma_f32_16x16x4_f32)",
 }
-CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm")
+CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm", "gemm_lat")
 DTYPE = {
     "fp32": "fp32",
     "f16x3": "fp32 via f16x3 (each fp32 operand = hi+lo fp16, products ah*bh+ah*bl+al*bh, fp32 accumulate)",

@@ -265,7 +265,15 @@ static void launch_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 
 void set_last_conv_kernel(const char* k);  // conv_x3.hip
 
+void set_last_conv_kernel(const char* k);                  // conv_x3.hip
+bool launch_gemm_lat(const ConvArgs& a, hipStream_t st);  // gemm_lat.hip
+
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st) {
+  // small latency-bound GEMMs / 1x1 convs: exact-fp32 whole-K kernel (fp32 and f16x3 modes)
+  if ((!a.wh || a.prec == 0) && launch_gemm_lat(a, st)) {
+    set_last_conv_kernel("gemm_lat");
+    return;
+  }
   if (a.wh) {
     launch_conv_x3(a, st);
     return;

@@ -221,11 +221,85 @@ __global__ __launch_bounds__(256) void mha_small_kernel(const float* __restrict_
   }
 }
 
+// One workgroup per (scene, head): the head's Lq x hd queries and Lk x hd keys / values are staged in
+// LDS with coalesced row loads (one global round trip instead of a dependent load chain per query
+// row), then all Lq x Lk scores, the row softmaxes and the P.V product run out of LDS. Same
+// arithmetic as mha_small_kernel (k-ordered dot, * scale, max / exp / sum / * 1/sum, j-ordered P.V).
+__global__ __launch_bounds__(256) void mha_head_kernel(const float* __restrict__ q, int64_t ldq,
+                                                       const float* __restrict__ k, const float* __restrict__ v,
+                                                       int64_t ldkv, float* __restrict__ out, int64_t ldo, int Lq,
+                                                       int Lk, int nh, int hd, int64_t qbs, int64_t kvbs, int64_t obs) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int hp = hd + 1;  // padded row pitch (conflict-free column walks)
+  float* Qs = sm;                  // [Lq][hp]
+  float* Ks = Qs + Lq * hp;        // [Lk][hp]
+  float* Vs = Ks + Lk * hp;        // [Lk][hd]
+  float* Ps = Vs + Lk * hd;        // [Lq][Lk + 1]
+  const int pp = Lk + 1;
+  const int h = blockIdx.x % nh, b = blockIdx.x / nh;
+  const float* qb = q + b * qbs + h * hd;
+  const float* kb = k + b * kvbs + h * hd;
+  const float* vb = v + b * kvbs + h * hd;
+  for (int t = threadIdx.x; t < Lq * hd; t += 256) {
+    const int i = t / hd, e = t - i * hd;
+    Qs[i * hp + e] = qb[(int64_t)i * ldq + e];
+  }
+  for (int t = threadIdx.x; t < Lk * hd; t += 256) {
+    const int j = t / hd, e = t - j * hd;
+    Ks[j * hp + e] = kb[(int64_t)j * ldkv + e];
+    Vs[j * hd + e] = vb[(int64_t)j * ldkv + e];
+  }
+  __syncthreads();
+  const float scale = 1.0f / sqrtf((float)hd);
+  for (int t = threadIdx.x; t < Lq * Lk; t += 256) {
+    const int i = t / Lk, j = t - i * Lk;
+    float d = 0.f;
+    for (int e = 0; e < hd; ++e) d += Qs[i * hp + e] * Ks[j * hp + e];
+    Ps[i * pp + j] = d * scale;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = wv; i < Lq; i += 4) {
+    float* pr = Ps + i * pp;
+    const float s0 = lane < Lk ? pr[lane] : -INFINITY;
+    const float s1 = lane + 64 < Lk ? pr[lane + 64] : -INFINITY;
+    float m = fmaxf(s0, s1);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const float e0 = lane < Lk ? expf(s0 - m) : 0.f;
+    const float e1 = lane + 64 < Lk ? expf(s1 - m) : 0.f;
+    float sum = e0 + e1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    const float inv = 1.f / sum;
+    if (lane < Lk) pr[lane] = e0 * inv;
+    if (lane + 64 < Lk) pr[lane + 64] = e1 * inv;
+  }
+  __syncthreads();
+  float* ob = out + b * obs + h * hd;
+  for (int t = threadIdx.x; t < Lq * hd; t += 256) {
+    const int i = t / hd, e = t - i * hd;
+    const float* pr = Ps + i * pp;
+    float acc = 0.f;
+    for (int j = 0; j < Lk; ++j) acc += pr[j] * Vs[j * hd + e];
+    ob[(int64_t)i * ldo + e] = acc;
+  }
+}
+
 void launch_mha_small(const float* q, int64_t ldq, const float* k, const float* v, int64_t ldkv, float* out,
                       int64_t ldo, int B, int Lq, int Lk, int nh, int hd, int64_t q_bstride, int64_t kv_bstride,
                       int64_t o_bstride, hipStream_t st) {
   if (Lk > 128 || Lk < 1) throw std::runtime_error("mha_small: 1 <= Lk <= 128 required");
+  const size_t lds = sizeof(float) * ((size_t)Lq * (hd + 1) + (size_t)Lk * (hd + 1) + (size_t)Lk * hd +
+                                      (size_t)Lq * (Lk + 1));
+  if (lds <= 64 * 1024) {
+    hipLaunchKernelGGL(mha_head_kernel, dim3(B * nh), dim3(256), lds, st, q, ldq, k, v, ldkv, out, ldo, Lq, Lk, nh,
+                       hd, q_bstride, kv_bstride, o_bstride);
+    DD_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int items = B * nh * Lq;
+
   hipLaunchKernelGGL(mha_small_kernel, dim3((items + 3) / 4), dim3(256), 0, st, q, ldq, k, v, ldkv, out, ldo, B, Lq,
                      Lk, nh, hd, q_bstride, kv_bstride, o_bstride);
   DD_HIP_CHECK(hipGetLastError());

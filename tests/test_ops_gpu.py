@@ -148,7 +148,8 @@ def test_conv2d_x6_flags_overflow(gpu):
 
 
 @pytest.mark.parametrize("M,K,N,relu", [(1, 256, 1024, False), (1280, 256, 256, True), (4096, 320, 256, True),
-                                        (600, 1024, 24, False), (77, 8, 256, False), (1280, 256, 1, False)])
+                                        (600, 1024, 24, False), (77, 8, 256, False), (1280, 256, 1, False),
+                                        (20, 512, 768, True), (4096, 512, 64, False), (4160, 256, 512, True)])
 def test_gemm(gpu, M, K, N, relu):
     a = rnd(M, K, seed=5)
     w = rnd(N, K, seed=6, scale=1.0 / np.sqrt(K))
