@@ -136,7 +136,7 @@ def main():
     conv_stats = {k: model.kernel_stats(k) for k in CONV_KERNELS}
     main_k = max(CONV_KERNELS, key=lambda k: conv_stats[k]["ms"])
     st = conv_stats[main_k]
-    other = {k: model.kernel_stats(k) for k in ("attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
+    other = {k: model.kernel_stats(k) for k in ("stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
                                                  "misc")}
     other.update({k: v for k, v in conv_stats.items() if k != main_k})
     model.set_profiling(False)

@@ -120,6 +120,47 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
   });
 }
 
+int dd_op_stem_pool_x3(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out,
+                       unsigned* flags, void* stream) {
+  return op_guard([&] {
+    const int Cin = 4, Cout = 64, K = 7 * 7 * Cin;
+    std::vector<float> hw((size_t)Cout * K);
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));
+    DD_HIP_CHECK(hipMemcpy(hw.data(), wgt, hw.size() * sizeof(float), hipMemcpyDeviceToHost));
+    Arena ar;
+    const SplitW x = prep_split(ar, hw.data(), Cout, K);
+    ar.upload();
+    ConvArgs a;
+    a.in = in;
+    a.in_sw = Cin;
+    a.in_sh = (int64_t)W * Cin;
+    a.in_sn = (int64_t)H * W * Cin;
+    a.H = H;
+    a.W = W;
+    a.Cin = Cin;
+    a.wgt = wgt;
+    a.ldb = K;
+    a.bias = bias;
+    a.Nimg = B;
+    a.Ho = (H + 6 - 7) / 2 + 1;
+    a.Wo = (W + 6 - 7) / 2 + 1;
+    a.Cout = Cout;
+    a.KH = a.KW = 7;
+    a.stride = 2;
+    a.pad = 3;
+    a.relu = 1;
+    a.prec = 0;
+    a.wh = reinterpret_cast<const uint16_t*>(ar.ptr(x.hi));
+    a.wl = reinterpret_cast<const uint16_t*>(ar.ptr(x.lo));
+    a.wsinv = ar.ptr(x.sinv);
+    a.ldh = x.ldh;
+    a.flags = flags;
+    const int hp = (a.Ho + 2 - 3) / 2 + 1, wp = (a.Wo + 2 - 3) / 2 + 1;
+    if (!launch_stem_pool(a, out, hp, wp, S(stream))) throw std::invalid_argument("stem_pool: shape not supported");
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));  // the split images die with `ar`
+  });
+}
+
 int dd_build_camera(const uint8_t* cams, int B, int src_h, int src_w, float* out, int out_h, int out_w,
                     void* stream) {
   return op_guard([&] {

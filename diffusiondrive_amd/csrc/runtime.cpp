@@ -466,9 +466,9 @@ class Model {
   }
 
   // conv on strided NHWC views
-  void conv(const Conv& c, const float* in, int64_t isn, int64_t ish, int64_t isw, int N, int H, int Wd, float* out,
-            int64_t osn, int64_t osh, int64_t osw, bool relu, const float* res = nullptr, int64_t rsn = 0,
-            int64_t rsh = 0, int64_t rsw = 0) {
+  ConvArgs conv_args(const Conv& c, const float* in, int64_t isn, int64_t ish, int64_t isw, int N, int H, int Wd,
+                     float* out, int64_t osn, int64_t osh, int64_t osw, bool relu, const float* res, int64_t rsn,
+                     int64_t rsh, int64_t rsw) {
     ConvArgs a;
     a.in = in;
     a.in_sn = isn;
@@ -497,8 +497,27 @@ class Model {
     a.pad = c.pad;
     a.relu = relu;
     use_split(a, c.x3);
+    return a;
+  }
+  void conv(const Conv& c, const float* in, int64_t isn, int64_t ish, int64_t isw, int N, int H, int Wd, float* out,
+            int64_t osn, int64_t osh, int64_t osw, bool relu, const float* res = nullptr, int64_t rsn = 0,
+            int64_t rsh = 0, int64_t rsw = 0) {
+    ConvArgs a = conv_args(c, in, isn, ish, isw, N, H, Wd, out, osn, osh, osw, relu, res, rsn, rsh, rsw);
     const double fl = 2.0 * N * a.Ho * a.Wo * (double)c.cout * c.k * c.k * c.cin_real;
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
+  }
+  // timm stem conv1 / bn1 / act1 + maxpool 3x3/2: one fused kernel (stem_pool.hip) in f16x3 mode,
+  // otherwise the conv into `stem` and the pool from it
+  void stem_and_pool(const Conv& c, const float* in4, int N, int H, int Wd, float* stem, float* pool, int hp, int wp) {
+    const int hs = (H + 2 * c.pad - c.k) / c.stride + 1, ws = (Wd + 2 * c.pad - c.k) / c.stride + 1;
+    ConvArgs a = conv_args(c, in4, (int64_t)H * Wd * c.cin, (int64_t)Wd * c.cin, c.cin, N, H, Wd, stem,
+                           (int64_t)hs * ws * c.cout, (int64_t)ws * c.cout, c.cout, true, nullptr, 0, 0, 0);
+    bool done = false;
+    const double fl = 2.0 * N * hs * ws * (double)c.cout * c.k * c.k * c.cin_real;
+    launch("stem_pool", fl, [&] { done = launch_stem_pool(a, pool, hp, wp, st); });
+    if (done) return;
+    conv_c(c, in4, N, H, Wd, stem, true);
+    launch("pool", 0, [&] { launch_maxpool3x3s2(stem, pool, N, hs, ws, c.cout, hp, wp, st); });
   }
   // contiguous NHWC conv; returns output spatial size
   void conv_c(const Conv& c, const float* in, int N, int H, int Wd, float* out, bool relu, const float* res = nullptr) {
@@ -666,11 +685,9 @@ class Model {
     float* pool_l = buf("lid_pool", (size_t)B * hl2 * wl2 * 64);
     fork();
     side([&] {
-      conv_c(lid.stem, lid4, B, HL, WL, stem_l, true);
-      launch("pool", 0, [&] { launch_maxpool3x3s2(stem_l, pool_l, B, hl, wl, 64, hl2, wl2, st); });
+      stem_and_pool(lid.stem, lid4, B, HL, WL, stem_l, pool_l, hl2, wl2);
     });
-    conv_c(img.stem, cam4, B, HC, WC, stem_i, true);
-    launch("pool", 0, [&] { launch_maxpool3x3s2(stem_i, pool_i, B, hi, wi, 64, hi2, wi2, st); });
+    stem_and_pool(img.stem, cam4, B, HC, WC, stem_i, pool_i, hi2, wi2);
 
     // ---- 4 scales: trunk stages (image on the main stream, LiDAR beside it) + GPT fusion
     float* xi = pool_i;

@@ -1,0 +1,236 @@
+// Fused ResNet stem: conv 7x7 / stride 2 / pad 3 (Cin 4: the camera's RGB or the LiDAR histogram,
+// zero-padded to 4 channels; Cout 64) + folded BatchNorm + ReLU + maxpool 3x3 / stride 2 / pad 1
+// (timm conv1 / bn1 / act1 / maxpool of both trunks, transfuser_backbone.py:23-33,50-55,175-192).
+//
+// The unfused path writes the 64-channel stem map (1.07 GB at B = 64 for the camera) and reads it
+// back for the pool; here a workgroup owns a PH x PW tile of POOLED outputs, computes the
+// (2PH+1) x (2PW+1) stem pixels under it (the pool windows overlap by one stem row / column, which
+// is recomputed: 16 %), keeps them in LDS and writes only the pooled map.
+//
+// Arithmetic: f16x3 as conv_x3.hip (fp32 operands split into fp16 hi + lo, products al*bh + ah*bl +
+// ah*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation, per-channel power-of-two weight scale undone
+// in the epilogue, non-finite accumulators raise DD_NUM_F16_OVERFLOW).
+//  * GEMM view per tile: M = stem pixels (297 -> 10 tiles of 32), N = 64 channels (2 tiles),
+//    K = 7 kh x 8 kw x 4 ch = 224 (kw = 7 is a zero tap): 14 k16 steps, each = one kernel row kh and
+//    four consecutive taps = 4 consecutive input pixels of that row.
+//  * A: the (4PH+7) x (4PW+8) input patch is split once into fp16 hi / lo images in LDS (8 B per
+//    pixel); a lane's 8-half fragment is the 2 input pixels (2sx - 3 + kw, kw = 4g + 2h, +1) of one
+//    row - one 16-B ds_read_b128 per image (the patch starts at an odd input column so every such
+//    pair is 16-B aligned).
+//  * B: the 64 x 224 weight images are loop-invariant: each wave keeps its 32-channel half as 14
+//    hi + 14 lo fragments in registers for the whole persistent loop over tiles.
+//  * Epilogue: scale, bias, ReLU into an LDS [pixel][64] fp32 stem tile (stem pixels outside the map
+//    are written as 0: every pool window holds at least one real pixel, all >= 0 after the ReLU, so
+//    0 stands in for the pool's -inf padding), then the 3 x 3 / 2 max over float4 channel quads and
+//    one 16-B store per pooled pixel quad.
+//  * Persistent grid (one 8-wave workgroup per CU, ~111 KB LDS); the next tile's input patch is
+//    loaded into registers while the current tile's MFMAs run.
+// Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.16 x recompute,
+// 224 / 196 K padding; HBM traffic = the input once (+ halo re-reads) + the pooled map.
+#include <cstdlib>
+
+#include "common.h"
+
+namespace ddmi {
+
+namespace {
+
+typedef _Float16 sp_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 sp_h4 __attribute__((ext_vector_type(4)));
+typedef float sp_f4 __attribute__((ext_vector_type(4)));
+typedef float sp_f16 __attribute__((ext_vector_type(16)));
+
+constexpr int PH = 4, PW = 16;                     // pooled outputs per tile
+constexpr int SH = 2 * PH + 1, SW = 2 * PW + 1;    // stem pixels per tile (9 x 33)
+constexpr int NSP = SH * SW;                       // 297
+constexpr int NMT = (NSP + 31) / 32;               // 10 M tiles
+constexpr int IH = 4 * PH + 7, IW = 4 * PW + 8;    // input pixels per tile (23 x 72; col 71 feeds only
+                                                   // the zero kw = 7 tap, but must be finite)
+constexpr int IP = IW;                             // LDS pitch in pixels (even)
+constexpr int KS = 14;                             // k16 steps
+constexpr int SOP = 64 + 4;                        // stem tile pitch (floats)
+constexpr int NT = 512;                            // threads (8 waves)
+constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread per tile
+constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
+constexpr int LDS_BYTES = 2 * IMG_BYTES + NMT * 32 * SOP * 4;
+
+__device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
+  hi = __builtin_convertvector(v, sp_h4);
+  const sp_f4 r = v - __builtin_convertvector(hi, sp_f4);
+  lo = __builtin_convertvector(r, sp_h4);
+}
+
+__global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__ in, int H, int W, int Hs, int Ws,
+                                                       int Hp, int Wp, const uint16_t* __restrict__ wh,
+                                                       const uint16_t* __restrict__ wl, int ldh,
+                                                       const float* __restrict__ wsinv,
+                                                       const float* __restrict__ bias, float alpha,
+                                                       float* __restrict__ out, unsigned* flags, int tiles_x,
+                                                       int tiles_y, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* in_hi = lds;
+  char* in_lo = lds + IMG_BYTES;
+  float* so = reinterpret_cast<float*>(lds + 2 * IMG_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, hl = lane >> 5;
+  const int nt = wave & 1, mg = wave >> 1;
+  const int co = nt * 32 + li;
+
+  // ---- loop-invariant B fragments of this wave's 32 channels (k = kh*28 + kw*4 + ci)
+  sp_h8 bh[KS], bl[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int kh = s >> 1, kw0 = 4 * (s & 1) + 2 * hl;
+    const int64_t o = (int64_t)co * ldh + kh * 28 + kw0 * 4;
+    const uint2 h0 = *reinterpret_cast<const uint2*>(wh + o);
+    const uint2 l0 = *reinterpret_cast<const uint2*>(wl + o);
+    uint2 h1 = make_uint2(0u, 0u), l1 = make_uint2(0u, 0u);
+    if (kw0 + 1 < 7) {
+      h1 = *reinterpret_cast<const uint2*>(wh + o + 4);
+      l1 = *reinterpret_cast<const uint2*>(wl + o + 4);
+    }
+    const uint4 hv = make_uint4(h0.x, h0.y, h1.x, h1.y), lv = make_uint4(l0.x, l0.y, l1.x, l1.y);
+    bh[s] = __builtin_bit_cast(sp_h8, hv);
+    bl[s] = __builtin_bit_cast(sp_h8, lv);
+  }
+  const float scl = wsinv[co] * alpha;
+  const float bia = bias ? bias[co] : 0.f;
+  bool bad = false;
+
+  auto tile_origin = [&](int t, int& b, int& py0, int& px0) {
+    const int tx = t % tiles_x, t2 = t / tiles_x;
+    px0 = tx * PW;
+    py0 = (t2 % tiles_y) * PH;
+    b = t2 / tiles_y;
+  };
+  sp_f4 pre[ILD];
+  auto load_patch = [&](int t) {
+    int b, py0, px0;
+    tile_origin(t, b, py0, px0);
+    const int iy0 = 4 * py0 - 5, ix0 = 4 * px0 - 5;
+#pragma unroll
+    for (int i = 0; i < ILD; ++i) {
+      const int e = tid + NT * i;
+      const int r = e / IW, c = e - (e / IW) * IW;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const bool ok = e < IH * IW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      pre[i] = ok ? *reinterpret_cast<const sp_f4*>(in + (((int64_t)b * H + iy) * W + ix) * 4)
+                  : (sp_f4){0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_patch = [&]() {
+#pragma unroll
+    for (int i = 0; i < ILD; ++i) {
+      const int e = tid + NT * i;
+      if (e < IH * IW) {
+        const int r = e / IW, c = e - (e / IW) * IW;
+        sp_h4 hi, lo;
+        sp_split4(pre[i], hi, lo);
+        *reinterpret_cast<sp_h4*>(in_hi + (r * IP + c) * 8) = hi;
+        *reinterpret_cast<sp_h4*>(in_lo + (r * IP + c) * 8) = lo;
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t < ntiles) load_patch(t);
+  for (; t < ntiles; t += gridDim.x) {
+    store_patch();
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x);  // lands under this tile's MFMAs
+
+    int b, py0, px0;
+    tile_origin(t, b, py0, px0);
+    const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;
+    // ---- stem GEMM: wave (nt, mg) takes M tiles mg, mg + 4, mg + 8
+    for (int m = mg; m < NMT; m += 4) {
+      const int p = min(m * 32 + li, NSP - 1);
+      const int ly = p / SW, lx = p - (p / SW) * SW;
+      const int base = (2 * ly) * IP + 2 * lx + 2 * hl;  // input pixel of (kh 0, kw 2h)
+      sp_f16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int off = (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
+        const sp_h8 ah = *reinterpret_cast<const sp_h8*>(in_hi + off);
+        const sp_h8 al = *reinterpret_cast<const sp_h8*>(in_lo + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+      }
+      // C/D layout: column (channel) li, row (pixel) (r & 3) + 8 (r >> 2) + 4 hl
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pr = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (pr < NSP) {
+          bad |= !__builtin_isfinite(acc[r]);
+          const int sy = sy0 + pr / SW, sx = sx0 + pr % SW;
+          float v = fmaxf(acc[r] * scl + bia, 0.f);
+          if ((unsigned)sy >= (unsigned)Hs || (unsigned)sx >= (unsigned)Ws) v = 0.f;
+          so[pr * SOP + co] = v;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 3 x 3 / 2 max pool over the stem tile: (pooled pixel, channel quad) items
+    for (int i = tid; i < PH * PW * 16; i += NT) {
+      const int q = i & 15, pp = i >> 4;
+      const int py = pp / PW, px = pp - (pp / PW) * PW;
+      const int gy = py0 + py, gx = px0 + px;
+      sp_f4 mx = *reinterpret_cast<const sp_f4*>(so + ((2 * py) * SW + 2 * px) * SOP + 4 * q);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const sp_f4 v = *reinterpret_cast<const sp_f4*>(so + ((2 * py + dy) * SW + 2 * px + dx) * SOP + 4 * q);
+          mx.x = fmaxf(mx.x, v.x);
+          mx.y = fmaxf(mx.y, v.y);
+          mx.z = fmaxf(mx.z, v.z);
+          mx.w = fmaxf(mx.w, v.w);
+        }
+      if (gy < Hp && gx < Wp) *reinterpret_cast<sp_f4*>(out + (((int64_t)b * Hp + gy) * Wp + gx) * 64 + 4 * q) = mx;
+    }
+    __syncthreads();  // the next tile overwrites the patch and the stem tile
+  }
+  if (bad && flags) atomicOr(flags, (unsigned)DD_NUM_F16_OVERFLOW);
+}
+
+}  // namespace
+
+// Returns false when the conv is not a 7x7 / s2 / p3, Cin 4, Cout 64 f16x3 stem on a contiguous NHWC4
+// input (the caller then runs the conv and the pool separately). DDMI_STEM_POOL=0 disables it.
+bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStream_t st) {
+  static const int on = getenv("DDMI_STEM_POOL") ? atoi(getenv("DDMI_STEM_POOL")) : 1;
+  if (!on || !a.wh || !a.wl || a.prec != 0 || !a.wsinv) return false;
+  if (a.KH != 7 || a.KW != 7 || a.stride != 2 || a.pad != 3 || a.Cin != 4 || a.Cout != 64 || a.batch != 1 || a.res ||
+      !a.relu)
+    return false;
+  if (a.in_sw != 4 || a.in_sh != (int64_t)a.W * 4 || a.in_sn != (int64_t)a.H * a.W * 4 || a.ldh < 196 || a.ldh % 4)
+    return false;
+  const int Hs = a.Ho, Ws = a.Wo;
+  if (Hp != (Hs + 2 - 3) / 2 + 1 || Wp != (Ws + 2 - 3) / 2 + 1) return false;
+  if ((reinterpret_cast<uintptr_t>(a.in) & 15) || (reinterpret_cast<uintptr_t>(pool_out) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.wh) & 7) || (reinterpret_cast<uintptr_t>(a.wl) & 7))
+    return false;
+  const int tiles_x = (Wp + PW - 1) / PW, tiles_y = (Hp + PH - 1) / PH;
+  const int64_t nt64 = (int64_t)a.Nimg * tiles_x * tiles_y;
+  if (nt64 >= (int64_t(1) << 31)) return false;
+  const int ntiles = (int)nt64;
+  int dev = 0, cus = 256;
+  DD_HIP_CHECK(hipGetDevice(&dev));
+  DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int grid = ntiles < cus ? ntiles : cus;
+  static bool attr = false;
+  if (!attr) {
+    DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    attr = true;
+  }
+  hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, a.H, a.W, Hs, Ws, Hp, Wp, a.wh,
+                     a.wl, (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
+  DD_HIP_CHECK(hipGetLastError());
+  return true;
+}
+
+}  // namespace ddmi

@@ -153,6 +153,11 @@ int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt
 int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
                     const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, int prec,
                     unsigned* flags, void* stream);
+/* Fused stem (replaces timm conv1 / bn1 / act1 / maxpool, transfuser_backbone.py:23-33,175-192): in (B,H,W,4)
+ * NHWC, wgt (64,7,7,4) OHWI with BN folded, bias (64) -> out (B,Hp,Wp,64) = maxpool3x3/2(relu(conv7x7/2(in) +
+ * bias)) on the f16x3 kernel (synchronous; weights split on the host as dd_create does). */
+int dd_op_stem_pool_x3(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out,
+                       unsigned* flags, void* stream);
 /* C (M,N) = A (M,K) . W(N,K)^T [+ bias] [+ res (M,N)] [relu] */
 int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,
                int relu, void* stream);

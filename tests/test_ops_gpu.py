@@ -278,3 +278,20 @@ def test_gpt_attention(gpu, B, T, C):
     qd = g(qkv)
     ok(gpu.dd_op_gpt_attention(qd.data_ptr(), out.data_ptr(), B, T, C, nh, None), gpu)
     close(out, ref, 2e-5)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 256), (1, 256, 256), (1, 40, 72), (2, 37, 50)])
+def test_stem_pool_f16x3(gpu, B, H, W):
+    """Fused stem conv 7x7/2 + bias + ReLU + maxpool 3x3/2 (transfuser_backbone.py:23-33) vs PyTorch fp64."""
+    x = rnd(B, 4, H, W, seed=41).abs()
+    x[:, 3] = 0.0  # the padded 4th input channel
+    w = rnd(64, 4, 7, 7, seed=42, scale=1.0 / np.sqrt(196))
+    b = rnd(64, seed=43)
+    ref = F.max_pool2d(F.relu(F.conv2d(x.double(), w.double(), b.double(), 2, 3)), 3, 2, 1)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win, bin_ = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b)
+    ok(gpu.dd_op_stem_pool_x3(xin.data_ptr(), B, H, W, win.data_ptr(), bin_.data_ptr(), out.data_ptr(),
+                              flags.data_ptr(), None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 3e-5)
+    assert int(flags.item()) == 0
