@@ -376,33 +376,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
   // ---- epilogue through LDS: the 256 x BN fp32 tile is parked as [pixel][BN], then every lane
   // finishes 16-B channel quads: weight scale, alpha, bias, residual, ReLU, one 16-B store.
   // C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
-  float* ct = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        ct[m * BN + (wn * TN + j) * 32 + li] = acc[i][j][r];
-      }
-  __syncthreads();
   constexpr int QN = BN / 4;  // channel quads per pixel
-  bool bad = false;
-  const int qn = tid % QN;    // fixed per thread (NT % QN == 0)
   static_assert(NT % QN == 0, "epilogue quads");
+  const int qn = tid % QN;    // fixed per thread (NT % QN == 0)
   const int nq = n0 + 4 * qn;
   const bool nv = nq < a.Cout;
-  x6f4 scl = {0.f, 0.f, 0.f, 0.f}, bia = {0.f, 0.f, 0.f, 0.f};
-  if (nv) {
-    scl = *reinterpret_cast<const x6f4*>(a.wsinv + nq) * a.alpha;
-    if (a.bias) bia = *reinterpret_cast<const x6f4*>(a.bias + nq);
-  }
   float* out = a.out + (int64_t)nimg * a.out_sn + nq;
   const float* res = a.res ? a.res + (int64_t)nimg * a.res_sn + nq : nullptr;
   const int osh = (int)a.out_sh, osw = (int)a.out_sw;
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
-  // every residual load in flight before the first use (latency-bound otherwise)
+  // the residual / scale / bias loads go out before the accumulators are parked, so their latency
+  // hides under the LDS staging and its barrier
   constexpr int IT = BM / (NT / QN);  // pixels per thread
   x6f4 rv[IT];
   int ooff[IT];
@@ -414,6 +398,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
     ooff[k] = ok ? oy * osh + ox * osw : -1;
     rv[k] = (res && ok) ? *reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw)) : (x6f4){0.f, 0.f, 0.f, 0.f};
   }
+  x6f4 scl = {0.f, 0.f, 0.f, 0.f}, bia = {0.f, 0.f, 0.f, 0.f};
+  if (nv) {
+    scl = *reinterpret_cast<const x6f4*>(a.wsinv + nq) * a.alpha;
+    if (a.bias) bia = *reinterpret_cast<const x6f4*>(a.bias + nq);
+  }
+  float* ct = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        ct[m * BN + (wn * TN + j) * 32 + li] = acc[i][j][r];
+      }
+  __syncthreads();
+  bool bad = false;
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     if (ooff[k] < 0) continue;

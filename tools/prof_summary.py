@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kclass(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     n = re.sub(r"^void\s+", "", n)
     n = n.replace("ddmi::", "")
     n = re.sub(r"<.*>", "", n)
