@@ -109,11 +109,14 @@ constexpr bool halo_in_window(int t, int D, int TA, bool first) {
 }  // namespace
 
 // TH x TW output pixels x BN channels per workgroup of WM x WN waves; B ring of NSLOT slots filled
-// D steps ahead (NSLOT >= D + 1).
+// D steps ahead (NSLOT >= D + 1). SH = 1: ONE halo buffer (the next chunk's halo is written after a
+// barrier that retires every wave's last read of the current one), so a 4-wave BN = 64 workgroup
+// fits twice per CU (66 KB of LDS) and one workgroup's prologue / epilogue runs beside the other's
+// MFMAs.
 // DBG (timing experiments only, results wrong): 1 no MFMA, 2 no B DMA, 4 no halo, 8 no fragment
 // reads, 16 no per-step barrier.
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int DBG = 0>
-__global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int DBG = 0>
+__global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = TH * TW;
@@ -131,8 +134,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
   static_assert(BPS >= 1 && (2 * BQ) % NW == 0 && BQ % BPS == 0, "B DMA split over the waves");
   constexpr int ALD = (HP * 8 + NT - 1) / NT;  // halo float4 loads per thread per chunk
   constexpr int TA = 1;                        // tap step at which the next chunk's halo is issued
-  constexpr int B_OFF = 2 * ABYTES;
-  constexpr int LDS_MAIN = 2 * ABYTES + NSLOT * BSLOT, LDS_EPI = BM * BN * 4;
+  constexpr int NHB = SH ? 1 : 2;          // halo buffers
+  constexpr int B_OFF = NHB * ABYTES;
+  constexpr int LDS_MAIN = NHB * ABYTES + NSLOT * BSLOT, LDS_EPI = BM * BN * 4;
   __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
 
@@ -160,17 +164,31 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
   const x6i4 rin = rsrc6(a.in);
 
   // ---- halo staging: thread element e = tid + NT i -> halo pixel e >> 3, channels 4 (e & 7) ..
-  int hofs[ALD];  // element offset of (pixel, 4q) at chunk 0, or -1 (zero fill)
-  int hwad[ALD];  // LDS byte offset (in a halo buffer) of the hi 8 bytes, -1 = no write
-#pragma unroll
-  for (int i = 0; i < ALD; ++i) {
+  // hofs: element offset of (pixel, 4q) at chunk 0, or -1 (zero fill); hwad: LDS byte offset (in a
+  // halo buffer) of the hi 8 bytes, -1 = no write. Kept in registers for 8-wave workgroups (ALD <= 6),
+  // recomputed per use by 4-wave ones (ALD = 11), whose register file is the limit.
+  constexpr bool HKEEP = ALD <= 6;
+  auto hofs_of = [&](int i) {
     const int e = tid + NT * i;
     const int px = e >> 3, q = e & 7;
     const int hy = px / P, hx = px - (px / P) * P;
     const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
     const bool in = px < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-    hofs[i] = in ? (int)(nimg * a.in_sn + iy * a.in_sh + ix * a.in_sw) + 4 * q : -1;
-    hwad[i] = px < HP ? px * 128 + ((((q >> 1) ^ (hx >> 1)) & 7) << 4) + ((q & 1) << 3) : -1;
+    return in ? (int)(nimg * a.in_sn + iy * a.in_sh + ix * a.in_sw) + 4 * q : -1;
+  };
+  auto hwad_of = [&](int i) {
+    const int e = tid + NT * i;
+    const int px = e >> 3, q = e & 7;
+    const int hx = px - (px / P) * P;
+    return px < HP ? px * 128 + ((((q >> 1) ^ (hx >> 1)) & 7) << 4) + ((q & 1) << 3) : -1;
+  };
+  int hofs[HKEEP ? ALD : 1], hwad[HKEEP ? ALD : 1];
+  if constexpr (HKEEP) {
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+      hofs[i] = hofs_of(i);
+      hwad[i] = hwad_of(i);
+    }
   }
   x6f4 hr[ALD];
   auto halo_issue = [&](int c) {
@@ -178,7 +196,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
     const bool cv = c < nchunks;
     const int co = c * 32;
 #pragma unroll
-    for (int i = 0; i < ALD; ++i) hr[i] = vload6(rin, (cv && hofs[i] >= 0) ? (uint32_t)(hofs[i] + co) * 4u : kOOB6);
+    for (int i = 0; i < ALD; ++i) {
+      const int ho = HKEEP ? hofs[HKEEP ? i : 0] : hofs_of(i);
+      hr[i] = vload6(rin, (cv && ho >= 0) ? (uint32_t)(ho + co) * 4u : kOOB6);
+    }
   };
   auto halo_tie = [&]() {  // after a wait: no use of the staged registers may move above it
 #pragma unroll
@@ -189,11 +210,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
     char* base = lds + buf * ABYTES;
 #pragma unroll
     for (int i = 0; i < ALD; ++i) {
-      if (hwad[i] < 0) continue;
+      const int hw = HKEEP ? hwad[HKEEP ? i : 0] : hwad_of(i);
+      if (hw < 0) continue;
       uint2 hi, lo;
       split4(hr[i], hi, lo);
-      *reinterpret_cast<uint2*>(base + hwad[i]) = hi;
-      *reinterpret_cast<uint2*>(base + (hwad[i] ^ 64)) = lo;
+      *reinterpret_cast<uint2*>(base + hw) = hi;
+      *reinterpret_cast<uint2*>(base + (hw ^ 64)) = lo;
     }
   };
 
@@ -264,7 +286,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
       for (int i = 0; i < TM; ++i) F.ah[i] = F.al[i] = (x6h8){};
       return;
     }
-    const char* abuf = lds + (c & 1) * ABYTES + kh * P * 128;
+    const char* abuf = lds + (SH ? 0 : (c & 1)) * ABYTES + kh * P * 128;
     const char* bbuf = lds + B_OFF + slot * BSLOT;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -346,7 +368,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
       // the halo of chunk c+1 was issued when step TA opened; younger: B issued at steps TA+1 .. 8
       wait_vm<(8 - TA) * BPS>();
       halo_tie();
-      halo_store((c + 1) & 1);
+      if constexpr (SH) {
+        // every wave's fragment reads of this chunk's halo (the F1 reads above) have returned
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        halo_store(0);
+      } else {
+        halo_store((c + 1) & 1);
+      }
     }
     constexpr int t1 = (t + 1) % 9;
     const int c1 = t == 8 ? c + 1 : c;
@@ -386,18 +414,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
   const int osh = (int)a.out_sh, osw = (int)a.out_sw;
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
   // the residual / scale / bias loads go out before the accumulators are parked, so their latency
-  // hides under the LDS staging and its barrier
+  // hides under the LDS staging and its barrier (when the per-thread residual fits beside the
+  // accumulators: 8 quads; 4-wave workgroups load it after the barrier)
   constexpr int IT = BM / (NT / QN);  // pixels per thread
+  constexpr bool EARLY = IT <= 8;
   x6f4 rv[IT];
   int ooff[IT];
+  auto load_res = [&]() {
 #pragma unroll
-  for (int k = 0; k < IT; ++k) {
-    const int p = tid / QN + k * (NT / QN);
-    const int oy = oy0 + p / TW, ox = ox0 + p % TW;
-    const bool ok = nv && oy < a.Ho && ox < a.Wo;
-    ooff[k] = ok ? oy * osh + ox * osw : -1;
-    rv[k] = (res && ok) ? *reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw)) : (x6f4){0.f, 0.f, 0.f, 0.f};
-  }
+    for (int k = 0; k < IT; ++k) {
+      const int p = tid / QN + k * (NT / QN);
+      const int oy = oy0 + p / TW, ox = ox0 + p % TW;
+      const bool ok = nv && oy < a.Ho && ox < a.Wo;
+      ooff[k] = ok ? oy * osh + ox * osw : -1;
+      rv[k] = (res && ok) ? *reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw)) : (x6f4){0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  if constexpr (EARLY) load_res();
   x6f4 scl = {0.f, 0.f, 0.f, 0.f}, bia = {0.f, 0.f, 0.f, 0.f};
   if (nv) {
     scl = *reinterpret_cast<const x6f4*>(a.wsinv + nq) * a.alpha;
@@ -414,6 +447,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
         ct[m * BN + (wn * TN + j) * 32 + li] = acc[i][j][r];
       }
   __syncthreads();
+  if constexpr (!EARLY) load_res();
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
@@ -434,21 +468,21 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvArgs a, int t
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int DBG = 0>
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int DBG = 0>
 static void launch_x6_one(const ConvArgs& a, hipStream_t st) {
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   const int n_sp = a.Nimg * tiles_x * tiles_y;
   const int ntn = (a.Cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, DBG>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0, st,
+  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, DBG>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0, st,
                      a, tiles_x, tiles_y, n_sp, ntn, a.Cin / 32);
   DD_HIP_CHECK(hipGetLastError());
 }
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT>
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
 static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
   static const int dbg = getenv("DDMI_X6_DBG") ? atoi(getenv("DDMI_X6_DBG")) : 0;
   switch (dbg) {
-#define X6D(V) case V: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, V>(a, st); break;
-    X6D(0) X6D(1) X6D(2) X6D(4) X6D(6) X6D(8) X6D(16) X6D(14) X6D(15) X6D(9)
+#define X6D(V) case V: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, V>(a, st); break;
+    X6D(0) X6D(1) X6D(2) X6D(4) X6D(8) X6D(16)
 #undef X6D
     default: throw std::runtime_error("bad DDMI_X6_DBG");
   }
@@ -475,18 +509,22 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
                                                : ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16));
   const bool bn128 = a.Cout > 64 && n_sp * ((a.Cout + 127) / 128) >= 256;
   static const int cfg = getenv("DDMI_X6_CFG") ? atoi(getenv("DDMI_X6_CFG")) : 0;
-#define X6(TH, TW, BN, WM, WN, D, NS) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS>(a, st)
+  // BN = 64 with Cin <= 64 (2 K chunks per tile: prologue / epilogue-heavy): 4-wave workgroups
+  // (wave tile 64 x 64) with one halo buffer, two per CU - 12 % faster on the 64-channel layers,
+  // 11 % slower at Cin = 256 (tools/micro/conv_bench); cfg 2 forces the 8-wave form, cfg 3 the 4-wave
+  const bool sh4 = cfg == 3 || (cfg != 2 && a.Cin <= 64);
+#define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   if (wide) {
     if (bn128) {
-      X6(8, 32, 128, 4, 2, 3, 4);
+      X6(8, 32, 128, 4, 2, 3, 4, 0);
     } else {
-      if (cfg == 1) X6(8, 32, 64, 4, 2, 8, 9); else X6(8, 32, 64, 4, 2, 2, 3);
+      if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else X6(8, 32, 64, 4, 2, 2, 3, 0);
     }
   } else {
     if (bn128) {
-      X6(16, 16, 128, 4, 2, 3, 4);
+      X6(16, 16, 128, 4, 2, 3, 4, 0);
     } else {
-      if (cfg == 1) X6(16, 16, 64, 4, 2, 8, 9); else X6(16, 16, 64, 4, 2, 2, 3);
+      if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else X6(16, 16, 64, 4, 2, 2, 3, 0);
     }
   }
 #undef X6
