@@ -438,42 +438,48 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   const float* res = a.res;
   const int osh = (int)a.out_sh, osw = (int)a.out_sw;
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
+  // rows (n, oh, ow) of fragment row group q of slab i
+  auto row_of = [&](int i, int q, int e, int& n, int& oh, int& ow) {
+    const int m = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh + e;
+    ow = m % a.Wo;
+    const int t2 = m / a.Wo;
+    oh = t2 % a.Ho;
+    n = t2 / a.Ho;
+    return m < M;
+  };
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    // this 32-row slab's residuals are all loaded before its first store: out may alias res (in
+    // place x += f(x)), so loads interleaved with stores would serialise on memory latency
+    float rv[4][4][TN];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int mbase = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh;
-      int ow = mbase % a.Wo;
-      int t2 = mbase / a.Wo;
-      int oh = t2 % a.Ho;
-      int n = t2 / a.Ho;
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = mbase + e;
-        if (m < M) {
-          float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
-          const float* rrow = res ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
+        int n, oh, ow;
+        const bool mv = row_of(i, q, e, n, oh, ow);
+        const float* rrow = (res && mv) ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            if (ncol[j] < a.Cout) {
-              const float acc_v = acc[i][j][q * 4 + e];
-              bad |= !__builtin_isfinite(acc_v);
-              float v = acc_v * scl_v[j] + bias_v[j];
-              if (rrow) v += rrow[ncol[j]];
-              if (a.relu) v = fmaxf(v, 0.f);
-              orow[ncol[j]] = v;
-            }
-          }
-        }
-        if (++ow == a.Wo) {
-          ow = 0;
-          if (++oh == a.Ho) {
-            oh = 0;
-            ++n;
+        for (int j = 0; j < TN; ++j) rv[q][e][j] = (rrow && ncol[j] < a.Cout) ? rrow[ncol[j]] : 0.f;
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int n, oh, ow;
+        if (!row_of(i, q, e, n, oh, ow)) continue;
+        float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (ncol[j] < a.Cout) {
+            const float acc_v = acc[i][j][q * 4 + e];
+            bad |= !__builtin_isfinite(acc_v);
+            float v = acc_v * scl_v[j] + bias_v[j] + rv[q][e][j];
+            if (a.relu) v = fmaxf(v, 0.f);
+            orow[ncol[j]] = v;
           }
         }
       }
-    }
   }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }

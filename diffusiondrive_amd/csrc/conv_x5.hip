@@ -17,9 +17,12 @@
 //    image, slot swizzle (row >> 2) & 3, read with ds_read_b128 as in conv_x3.
 //  * Conv zero padding and ragged M / N / K edges: out-of-range buffer offsets (>= num_records)
 //    make the DMA deposit zeros; no per-element branches.
-//  * Two LDS stages; one barrier per 32-wide K chunk: wait for this wave's DMAs (vmcnt(0)), barrier
-//    (every wave's DMAs of chunk kc have landed and every wave has finished reading chunk kc-1), issue
-//    chunk kc+1's DMAs into the freed stage, then the chunk-kc MFMAs run while they fly.
+//  * NS LDS stages, chunks issued NS-1 ahead; one barrier per 32-wide K chunk. Every DMA is inline
+//    asm, so the compiler's waitcnt pass (which cannot tell an LDS-DMA target from the stage being
+//    read and otherwise drains vmcnt(0) before the first ds_read after an issue - the serialisation
+//    that held this kernel at conv_x3's speed) never sees them; the kernel waits itself with the exact
+//    count: at chunk kc, vmcnt((NS-2) * DMAs per chunk) = this wave's chunk kc has landed, then the
+//    barrier (every wave's has, and every wave finished reading the stage chunk kc+NS-1 refills).
 //  * 256 x 256 / 256 x 128 / 256 x 64 tiles (8 / 8 / 4 waves): 64 KB of operands per 32-deep K chunk
 //    feed 384 MFMAs at 256 x 256 - half the L2 bytes per MFMA of conv_x3's 128 x 128.
 //  * XCD-aware bijective tile remap; fused epilogue (per-channel weight scale, alpha, bias,
@@ -36,17 +39,33 @@ typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 half2_v __attribute__((ext_vector_type(2)));
 typedef float float2_v __attribute__((ext_vector_type(2)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int KC = 32;                 // K chunk
 constexpr uint32_t kOOB5 = 0x80000000u;
 
-__device__ inline __amdgpu_buffer_rsrc_t rsrc5(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)kOOB5, 0x00020000);
+typedef int x5i4 __attribute__((ext_vector_type(4)));
+
+__device__ inline x5i4 rsrc5a(const void* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  x5i4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xffffu);  // stride 0
+  r.z = (int)kOOB5;                             // num_records: offsets >= 2^31 read as zero
+  r.w = 0x00020000;
+  return r;
 }
 
-__device__ inline void dma16(__amdgpu_buffer_rsrc_t r, const char* lds_wave_base, uint32_t byte_off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_wave_base, 16, byte_off, 0, 0, 0);
+// 16 B per lane from global (buffer offset voff) into LDS at m0 + 16 * lane (m0 = wave base),
+// invisible to the compiler's vmcnt bookkeeping (see the header)
+__device__ inline void dma16(x5i4 rsrc, uint32_t lds_wave, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds_wave), "v"(voff), "s"(rsrc)
+               : "memory");
+}
+
+template <int N>
+__device__ inline void chunk_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
 // 8 fp32 -> hi / lo fp16 fragments (RNE twice)
@@ -66,7 +85,7 @@ __device__ inline void split8(const float4& p, const float4& q, half8_t& hi, hal
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE>
+template <int WM, int WN, int TM, int TN, int MODE, int NS>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 (scalar tap walk, per-row tap masks); MODE 0: generic K.
@@ -80,7 +99,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   constexpr int B_IN = BN / 16 / NW;  // B DMA instructions per wave per chunk and image (16 rows x 64 B)
   static_assert(A_IN >= 1 && BM % (8 * NW) == 0, "A rows per wave");
   static_assert(B_IN >= 1 && BN % (16 * NW) == 0, "B rows per wave");
-  __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
+  static_assert(NS >= 2 && NS * STAGE <= 160 * 1024, "stages");
+  constexpr int DPC = A_IN + 2 * B_IN;  // DMA instructions per wave per chunk
+  __shared__ __attribute__((aligned(1024))) char lds[NS * STAGE];
+  const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -96,9 +118,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   const int m0 = mt_idx * BM;
   const int n0 = nt_idx * BN;
 
-  const __amdgpu_buffer_rsrc_t rin = rsrc5(a.in);
-  const __amdgpu_buffer_rsrc_t rwh = rsrc5(a.wh);
-  const __amdgpu_buffer_rsrc_t rwl = rsrc5(a.wl);
+  const x5i4 rin = rsrc5a(a.in);
+  const x5i4 rwh = rsrc5a(a.wh);
+  const x5i4 rwl = rsrc5a(a.wl);
   const int in_sh = (int)a.in_sh, in_sw = (int)a.in_sw;
   const int ldh = (int)a.ldh;
   const int Kp = (K + 7) & ~7;
@@ -150,12 +172,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
 
   int t_tap = 0, t_ci = 0, t_kw = 0, t_off = 0;  // MODE 1 scalar tap walk (chunk order)
   auto issue = [&](int buf, int k0) {
-    char* st = lds + buf * STAGE;
+    const uint32_t st = lds_u32 + buf * STAGE;
     if constexpr (MODE == 1) {
 #pragma unroll
       for (int q = 0; q < A_IN; ++q) {
         const bool ok = t_tap < 32 && ((amask[q] >> (t_tap & 31)) & 1u);
-        dma16(rin, st + (a_rbase + q * 8) * 128, ok ? (uint32_t)(abase[q] + t_off) * 4u : kOOB5);
+        dma16(rin, __builtin_amdgcn_readfirstlane(st + (a_rbase + q * 8) * 128), ok ? (uint32_t)(abase[q] + t_off) * 4u : kOOB5);
       }
       t_ci += KC;
       t_off += KC;
@@ -178,14 +200,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
         const int kw = tap - kh * a.KW;
         const int ih = aih0[q] + kh, iw = aiw0[q] + kw;
         const bool ok = kk < K && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        dma16(rin, st + (a_rbase + q * 8) * 128, ok ? (uint32_t)(abase[q] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB5);
+        dma16(rin, __builtin_amdgcn_readfirstlane(st + (a_rbase + q * 8) * 128),
+              ok ? (uint32_t)(abase[q] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB5);
       }
     }
 #pragma unroll
     for (int q = 0; q < B_IN; ++q) {
       const uint32_t off = (bok[q] && k0 + bkb[q] < Kp) ? boff[q] + (uint32_t)k0 * 2u : kOOB5;
-      dma16(rwh, st + AB + (b_rbase + q * 16) * 64, off);
-      dma16(rwl, st + AB + BB + (b_rbase + q * 16) * 64, off);
+      dma16(rwh, __builtin_amdgcn_readfirstlane(st + AB + (b_rbase + q * 16) * 64), off);
+      dma16(rwl, __builtin_amdgcn_readfirstlane(st + AB + BB + (b_rbase + q * 16) * 64), off);
     }
   };
 
@@ -217,11 +240,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   }
 
   const int nk = (K + KC - 1) / KC;
-  issue(0, 0);
+  // prologue: chunks 0 .. NS-2 (the MODE 1 tap walk advances in chunk order: issue order = k order)
+#pragma unroll
+  for (int u = 0; u < NS - 1; ++u) issue(u, u * KC);
+  int cur = 0;  // stage of chunk kc
   for (int kc = 0; kc < nk; ++kc) {
-    __syncthreads();  // (vmcnt(0) first: LDS-DMA is outstanding) chunk kc landed; stage (kc+1)&1 is free
-    issue((kc + 1) & 1, (kc + 1) * KC);
-    const char* st = lds + (kc & 1) * STAGE;
+    // this wave's DMAs of chunk kc have landed (NS-2 younger chunks may fly), every wave's have
+    // (barrier), and every wave finished reading chunk kc-1, whose stage is refilled below
+    chunk_barrier<(NS - 2) * DPC>();
+    int nxt = cur + NS - 1;
+    if (nxt >= NS) nxt -= NS;
+    issue(nxt, (kc + NS - 1) * KC);
+    const char* st = lds + cur * STAGE;
+    if (++cur == NS) cur = 0;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       half8_t ah[TM], al[TM], bh[TN], bl[TN];
@@ -253,7 +284,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
     }
   }
-  __syncthreads();  // drain the trailing (all-OOB) DMA before the block retires
+  chunk_barrier<0>();  // drain the trailing (all-OOB) DMAs before the block retires
 
   // ---- fused epilogue (as conv_x3). C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
   bool bad = false;
@@ -270,71 +301,85 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   const float* res = a.res;
   const int osh = (int)a.out_sh, osw = (int)a.out_sw;
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
+  // rows (n, oh, ow) of fragment row group q of slab i
+  auto row_of = [&](int i, int q, int e, int& n, int& oh, int& ow) {
+    const int m = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh + e;
+    ow = m % a.Wo;
+    const int t2 = m / a.Wo;
+    oh = t2 % a.Ho;
+    n = t2 / a.Ho;
+    return m < M;
+  };
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    // this 32-row slab's residuals are all loaded before its first store: out may alias res (in
+    // place x += f(x)), so loads interleaved with stores would serialise on memory latency
+    float rv[4][4][TN];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int mbase = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh;
-      int ow = mbase % a.Wo;
-      int t2 = mbase / a.Wo;
-      int oh = t2 % a.Ho;
-      int n = t2 / a.Ho;
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = mbase + e;
-        if (m < M) {
-          float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
-          const float* rrow = res ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
+        int n, oh, ow;
+        const bool mv = row_of(i, q, e, n, oh, ow);
+        const float* rrow = (res && mv) ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            if (ncol[j] < a.Cout) {
-              const float acc_v = acc[i][j][q * 4 + e];
-              bad |= !__builtin_isfinite(acc_v);
-              float v = acc_v * scl_v[j] + bias_v[j];
-              if (rrow) v += rrow[ncol[j]];
-              if (a.relu) v = fmaxf(v, 0.f);
-              orow[ncol[j]] = v;
-            }
-          }
-        }
-        if (++ow == a.Wo) {
-          ow = 0;
-          if (++oh == a.Ho) {
-            oh = 0;
-            ++n;
+        for (int j = 0; j < TN; ++j) rv[q][e][j] = (rrow && ncol[j] < a.Cout) ? rrow[ncol[j]] : 0.f;
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int n, oh, ow;
+        if (!row_of(i, q, e, n, oh, ow)) continue;
+        float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (ncol[j] < a.Cout) {
+            const float acc_v = acc[i][j][q * 4 + e];
+            bad |= !__builtin_isfinite(acc_v);
+            float v = acc_v * scl_v[j] + bias_v[j] + rv[q][e][j];
+            if (a.relu) v = fmaxf(v, 0.f);
+            orow[ncol[j]] = v;
           }
         }
       }
-    }
   }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int NS>
 static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int ntm = (M + BM - 1) / BM;
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
   if (a.Cin % KC == 0 && a.KH * a.KW <= 32)
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
   else
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
   DD_HIP_CHECK(hipGetLastError());
 }
 
-// Returns false when the shape is better served by conv_x3 (small grids).
+// Returns false when the shape is better served by conv_x3 (grids too small to fill the chip).
+// Tiles: 256 x 256 with 2 stages (128 KB), 256 x 128 / 256 x 64 with 3 (144 / 96 KB).
+// DDMI_X5_WIDE=1 also routes the Cout > 128 grids that only fill the chip at 256 x 128, and the
+// mid-size GEMMs at 128 x 128 (4 waves, 3 stages): measured slower than conv_x3's 128 x 128 /
+// 64 x 64 on the GPT shapes (tools/micro/gemm_x3_bench.py), so off by default.
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
-  const int64_t m256 = (M + 255) / 256;
+  static const int mode = getenv("DDMI_X5_WIDE") ? atoi(getenv("DDMI_X5_WIDE")) : 0;
+  const int64_t m256 = (M + 255) / 256, m128 = (M + 127) / 128;
+  const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;
   if (a.Cout <= 64) {
     if (m256 < 256) return false;
-    launch_x5_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64, 4 waves
-  } else if (a.Cout <= 128) {
-    if (m256 < 256) return false;
-    launch_x5_cfg<4, 2, 2, 2>(a, M, K, st);  // 256 x 128, 8 waves
+    launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st);  // 256 x 64, 4 waves
+  } else if (a.Cout > 128 && m256 * n256 >= 256) {
+    launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);  // 256 x 256, 8 waves
+  } else if ((a.Cout <= 128 || mode) && m256 * n128 >= 256) {
+    launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);  // 256 x 128, 8 waves
+  } else if (mode && m128 * n128 >= 256 && K >= 128) {
+    launch_x5_cfg<2, 2, 2, 2, 3>(a, M, K, st);  // 128 x 128, 4 waves
   } else {
-    if (m256 * ((a.Cout + 255) / 256) < 256) return false;
-    launch_x5_cfg<4, 2, 2, 4>(a, M, K, st);  // 256 x 256, 8 waves
+    return false;
   }
   return true;
 }

@@ -87,6 +87,11 @@ def test_conv2d(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     (16, 64, 64, 36, 200, 3, 1, 1, True, False),  # generic K path, ragged N in a 256-wide tile
     (1, 518, 518, 4, 64, 7, 2, 3, True, False),   # stem geometry (7x7/s2 on 4 padded channels)
     (3, 90, 250, 64, 256, 3, 2, 1, False, False), # stride 2, ragged M
+    (1, 128, 128, 64, 512, 1, 1, 0, True, True),  # 256 x 128 tiles (3 stages) for Cout > 128
+    (1, 64, 128, 128, 512, 1, 1, 0, False, True), # 128 x 128 tiles (4 waves, 3 stages)
+    (1, 70, 130, 160, 400, 1, 1, 0, False, True), # 128 x 128 tiles, ragged M and N
+    (1, 64, 128, 132, 512, 1, 1, 0, True, False), # 128 x 128 tiles, generic K (Cin % 32 != 0)
+    (1, 256, 256, 64, 256, 3, 2, 1, True, False), # 128 x 128 tiles, 3x3 stride-2 tap walk
     # 3x3 / stride 1 convs take the halo-reuse direct kernel (conv_x6.hip)
     (2, 8, 40, 128, 192, 3, 1, 1, True, True),    # 8 x 32 tiles, ragged W, BN 64 x 3
     (1, 12, 70, 64, 100, 3, 1, 1, False, True),   # 8 x 32 tiles ragged in H and W, ragged N
