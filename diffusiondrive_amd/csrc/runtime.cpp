@@ -379,21 +379,21 @@ class Model {
   }
   // profiled runs stay on one stream: per-launch event timing needs launches that do not overlap
   bool sides() const { return use_side && !profiling; }
-  void fork() {
+  void fork(hipStream_t to = nullptr) {
     if (!sides()) return;
     hipEvent_t e = fj_event();
     DD_HIP_CHECK(hipEventRecord(e, st_main));
-    DD_HIP_CHECK(hipStreamWaitEvent(st_side, e, 0));
+    DD_HIP_CHECK(hipStreamWaitEvent(to ? to : st_side, e, 0));
   }
-  void join() {
+  void join(hipStream_t from = nullptr) {
     if (!sides()) return;
     hipEvent_t e = fj_event();
-    DD_HIP_CHECK(hipEventRecord(e, st_side));
+    DD_HIP_CHECK(hipEventRecord(e, from ? from : st_side));
     DD_HIP_CHECK(hipStreamWaitEvent(st_main, e, 0));
   }
   template <class F>
-  void side(F&& f) {
-    st = sides() ? st_side : st_main;
+  void side(F&& f, hipStream_t on = nullptr) {
+    st = sides() ? (on ? on : st_side) : st_main;
     try {
       f();
     } catch (...) {
@@ -713,6 +713,8 @@ class Model {
     // stream beside the FPN / bev_proj / value_proj chain below
     const int NQ = 31;
     float* q = buf("query_out", (size_t)B * NQ * d);
+    float* egos[2];
+    float* akv[2];
     fork();
     side([&] {
       launch("misc", 0, [&] { launch_broadcast_rows(W(q_emb), NQ, q, B * NQ, d, st); });
@@ -741,6 +743,17 @@ class Model {
         gemm(w.l1, q, d, MQ, ff, 1024, true);
         gemm(w.l2, ff, 1024, MQ, tmp, d, false, q, d);
         ln(w.n3, tmp, d, q, d, MQ);
+      }
+      // per decoder layer, step-invariant (exact hoists): ego cross-attention over ONE key =
+      // out_proj(v_proj(ego)); agent K / V projections
+      for (int l = 0; l < 2; ++l) {
+        const DiffLayerW& w = dl[l];
+        float* e1 = buf("ego_v" + std::to_string(l), (size_t)B * d);
+        gemm_g(w.eg_v, q, (int64_t)NQ * d, d, B, 1, e1, d, d);
+        egos[l] = buf("ego_out" + std::to_string(l), (size_t)B * d);
+        gemm(w.eg_out, e1, d, B, egos[l], d);
+        akv[l] = buf("agent_kv" + std::to_string(l), (size_t)B * 30 * 2 * d);
+        gemm_g(w.ag_kv, q + d, (int64_t)NQ * d, d, B, 30, akv[l], (int64_t)30 * 2 * d, 2 * d);
       }
     });
 
@@ -781,7 +794,9 @@ class Model {
     gemm(bevproj, cross_in, CC, MB, cross, d, true);
     ln(bevproj_ln, cross, d, cross, d, MB);
 
-    // value_proj for both decoder layers (main stream, beside the tf decoder), then join
+    // value_proj for both decoder layers (main stream, beside the tf decoder), then join. (Layer 1's
+    // on a third stream beside the first trajectory-head layer was measured: the graph put it on
+    // the hardware queue of layer 0's and the head behind it - no overlap.)
     const int R = B * Q;  // trajectory query rows
     float* vals[2];
     for (int l = 0; l < 2; ++l) {
@@ -789,7 +804,6 @@ class Model {
       conv_c(dl[l].vproj, cross, B, HB, WB, vals[l], true);
     }
     join();
-    const float* ego = q;          // row 0 of each scene
     const float* agents = q + d;   // rows 1..30
 
     // ---- optional heads (off the waypoint path), on the side stream beside the trajectory head
@@ -820,17 +834,6 @@ class Model {
     });
 
     // ---- trajectory head (TrajectoryHead.forward_test, :578-641)
-    float* egos[2];
-    float* akv[2];
-    for (int l = 0; l < 2; ++l) {
-      const DiffLayerW& w = dl[l];
-      float* e1 = buf("ego_v" + std::to_string(l), (size_t)B * d);
-      gemm_g(w.eg_v, ego, (int64_t)NQ * d, d, B, 1, e1, d, d);
-      egos[l] = buf("ego_out" + std::to_string(l), (size_t)B * d);
-      gemm(w.eg_out, e1, d, B, egos[l], d);
-      akv[l] = buf("agent_kv" + std::to_string(l), (size_t)B * 30 * 2 * d);
-      gemm_g(w.ag_kv, agents, (int64_t)NQ * d, d, B, 30, akv[l], (int64_t)30 * 2 * d, 2 * d);
-    }
     float* imgx = buf("ddim_img", (size_t)R * P * 2);
     const bool vanilla = schedule == DD_SCHED_VANILLA;
     {
