@@ -77,7 +77,7 @@ def main():
     for name, s, e, gx, gz in rows:
         cls[kclass(name)][0] += 1
         cls[kclass(name)][1] += (e - s) / 1e3
-        short = re.sub(r"\(.*", "", name).replace("void ", "").replace("ddmi::", "")
+        short = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "")).replace("void ", "").replace("ddmi::", "")
         inst[short][0] += 1
         inst[short][1] += (e - s) / 1e3
     total_us = sum(v[1] for v in cls.values())
