@@ -61,6 +61,12 @@ struct ConvArgs {
   int64_t ldh = 0;
   unsigned* flags = nullptr;
   int prec = 0;  // 0 = f16x3 (wh / wl fp16 hi / lo), 1 = bf16 (wh = bf16 image, one product)
+  // Gathered output rows (conv_x3 MODE 1 only): output row m (launch geometry Nimg = 1, Ho = M,
+  // Wo = 1, compact rows out + m * out_sh) is the conv at input-geometry pixel rowmap[m] =
+  // n * H * W + oh * W + ow (stride 1, Ho = H, Wo = W), or a don't-care row when rowmap[m] < 0.
+  // rowmap_nimg = images in the input (operand-extent check).
+  const int* rowmap = nullptr;
+  int rowmap_nimg = 0;
 };
 constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
@@ -127,6 +133,13 @@ void launch_timestep_embed(float t, float* out, int dim, hipStream_t st);
 void launch_bev_sample_attn(const float* logits, const float* pts, const float* value, float* out,
                             int B, int Q, int P, int Hv, int Wv, int C, float inv_max_x,
                             float inv_max_y, hipStream_t st);
+// Gathered form (decoder.hip): the (B*Q*P*4) tap pixels (or -1) of the points, and the sampling
+// attention over a compact (B*Q*P*4, C) value array holding the conv at those taps.
+void launch_bev_tap_rows(const float* pts, int* rows, int B, int Q, int P, int Hv, int Wv, float inv_max_x,
+                         float inv_max_y, hipStream_t st);
+void launch_bev_sample_attn_gathered(const float* logits, const float* pts, const float* vrows, float* out, int B,
+                                     int Q, int P, int Hv, int Wv, int C, float inv_max_x, float inv_max_y,
+                                     hipStream_t st);
 // Small multi-head attention: out[b,i,h*hd+d] = sum_j softmax_j(q.k / sqrt(hd)) v. Lk <= 128, hd <= 64.
 void launch_mha_small(const float* q, int64_t ldq, const float* k, const float* v, int64_t ldkv,
                       float* out, int64_t ldo, int B, int Lq, int Lk, int nh, int hd,

@@ -270,7 +270,8 @@ bool launch_gemm_lat(const ConvArgs& a, hipStream_t st);  // gemm_lat.hip
 
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st) {
   // small latency-bound GEMMs / 1x1 convs: exact-fp32 whole-K kernel (fp32 and f16x3 modes)
-  if ((!a.wh || a.prec == 0) && launch_gemm_lat(a, st)) {
+  if (a.rowmap && !a.wh) throw std::runtime_error("conv_gemm: gathered rows need the f16x3 kernel (conv_x3)");
+  if (!a.rowmap && (!a.wh || a.prec == 0) && launch_gemm_lat(a, st)) {
     set_last_conv_kernel("gemm_lat");
     return;
   }

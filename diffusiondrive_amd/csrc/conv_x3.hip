@@ -107,10 +107,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     const int m = m0 + (tid >> 3) + (NT / 8) * i;
     const bool v = m < M;
     const int mm = v ? m : 0;
-    const int ow = mm % a.Wo;
+    int ow = mm % a.Wo;
     const int t2 = mm / a.Wo;
-    const int oh = t2 % a.Ho;
-    const int n = t2 / a.Ho;
+    int oh = t2 % a.Ho;
+    int n = t2 / a.Ho;
+    bool rv = v;
+    if (MODE == 1 && a.rowmap) {
+      // gathered rows: the pixel comes from the row map (stride 1: output geometry = input's)
+      const int px = v ? a.rowmap[m] : -1;
+      rv = px >= 0;
+      const int pp = rv ? px : 0;
+      ow = pp % a.W;
+      oh = (pp / a.W) % a.H;
+      n = pp / (a.W * a.H);
+    }
     const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
     if constexpr (MODE == 1) {
       // element offset of tap (0, 0) channel kq*4, and bit t set iff tap t reads inside the image
@@ -120,7 +130,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
         for (int kw = 0; kw < a.KW; ++kw)
           if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
             mk |= 1u << (kh * a.KW + kw);
-      amask[i] = v ? mk : 0u;
+      amask[i] = rv ? mk : 0u;
     } else {
       abase[i] = n * (int)a.in_sn;
       aih0[i] = v ? ih0 : -(1 << 28);
@@ -556,7 +566,10 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   const int K = a.KH * a.KW * a.Cin;
   if (a.ldh < K) throw std::runtime_error("conv_x3: ldh < K");
   if (M == 0 || a.Cout == 0) return;
-  const int64_t in_extent = (int64_t)(a.Nimg - 1) * a.in_sn + (int64_t)(a.H - 1) * a.in_sh +
+  if (a.rowmap && (a.stride != 1 || a.Cin % BK != 0 || a.KH * a.KW > 32 || a.Nimg != 1 || a.Wo != 1 ||
+                   a.rowmap_nimg < 1 || a.prec != 0))
+    throw std::runtime_error("conv_x3: gathered rows need a stride-1 f16x3 MODE-1 conv into Nimg=1, Wo=1");
+  const int64_t in_extent = (int64_t)((a.rowmap ? a.rowmap_nimg : a.Nimg) - 1) * a.in_sn + (int64_t)(a.H - 1) * a.in_sh +
                             (int64_t)(a.W - 1) * a.in_sw + a.Cin;
   if (in_extent * 4 >= (int64_t)kOOB || (int64_t)a.Cout * a.ldh * 2 >= (int64_t)kOOB)
     throw std::runtime_error("conv_x3: operand extent >= 2 GiB (split the batch)");
@@ -565,6 +578,11 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   // default f16x3 path: 3x3 stride-1 convs on the halo-reuse direct kernel (conv_x6.hip), other
   // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
   static const int use_x6 = getenv("DDMI_X6") ? atoi(getenv("DDMI_X6")) : 1;
+  if (a.rowmap) {
+    g_last_conv = "conv_x3";
+    launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);  // 128 x 128
+    return;
+  }
   if (use_x6 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x6(a, st)) {
     g_last_conv = "conv_x6";
     return;

@@ -163,6 +163,117 @@ void launch_bev_sample_attn(const float* logits, const float* pts, const float* 
   DD_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------- gathered value rows for the BEV sampling
+// value_proj is a 3x3 conv over the whole 64x64 BEV map (blocks.py:68-76,114), but grid_sample reads it
+// at only B x Q x P x 4 bilinear taps (:115-122). The gathered form evaluates the conv at those taps:
+// bev_tap_rows writes, per (scene, query, point, tap), the map pixel the tap reads (same ix / iy
+// arithmetic as bev_sample_attn) or -1 when zero padding applies; conv_x3 evaluates the conv at those
+// rows (ConvArgs::rowmap) into a compact (B*Q*P*4, C) array; bev_sample_attn_gathered then reads
+// tap t of point p of item from row (item * P + p) * 4 + t. Tap order: nw, ne, sw, se.
+__device__ inline void bev_tap_geometry(const float* pts, int64_t ip, int Hv, int Wv, float inv_max_x,
+                                        float inv_max_y, int& x0, int& y0, float wt[4]) {
+  const float tx = pts[ip * 2 + 0];
+  const float ty = pts[ip * 2 + 1];
+  const float gx = ty * inv_max_x;  // grid x (width) <- trajectory y  (blocks.py:101-108)
+  const float gy = tx * inv_max_y;  // grid y (height) <- trajectory x
+  const float ix = ((gx + 1.f) * (float)Wv - 1.f) / 2.f;
+  const float iy = ((gy + 1.f) * (float)Hv - 1.f) / 2.f;
+  const float fx = floorf(ix), fy = floorf(iy);
+  x0 = (int)fx;
+  y0 = (int)fy;
+  const int x1 = x0 + 1, y1 = y0 + 1;
+  wt[0] = ((float)x1 - ix) * ((float)y1 - iy);
+  wt[1] = (ix - (float)x0) * ((float)y1 - iy);
+  wt[2] = ((float)x1 - ix) * (iy - (float)y0);
+  wt[3] = (ix - (float)x0) * (iy - (float)y0);
+}
+
+__global__ __launch_bounds__(256) void bev_tap_rows_kernel(const float* __restrict__ pts, int* __restrict__ rows,
+                                                           int B, int Q, int P, int Hv, int Wv, float inv_max_x,
+                                                           float inv_max_y) {
+  const int64_t ip = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ip >= (int64_t)B * Q * P) return;
+  const int b = (int)(ip / ((int64_t)Q * P));
+  int x0, y0;
+  float wt[4];
+  bev_tap_geometry(pts, ip, Hv, Wv, inv_max_x, inv_max_y, x0, y0, wt);
+  int4 r;
+  auto px = [&](int yy, int xx) {
+    return ((unsigned)yy < (unsigned)Hv && (unsigned)xx < (unsigned)Wv) ? (b * Hv + yy) * Wv + xx : -1;
+  };
+  r.x = px(y0, x0);
+  r.y = px(y0, x0 + 1);
+  r.z = px(y0 + 1, x0);
+  r.w = px(y0 + 1, x0 + 1);
+  *reinterpret_cast<int4*>(rows + ip * 4) = r;
+}
+
+__global__ __launch_bounds__(256) void bev_sample_attn_gathered_kernel(
+    const float* __restrict__ logits, const float* __restrict__ pts, const float* __restrict__ vrows,
+    float* __restrict__ out, int B, int Q, int P, int Hv, int Wv, int C, float inv_max_x, float inv_max_y) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= B * Q) return;
+  const float* lg = logits + (int64_t)item * P;
+  float mx = -INFINITY;
+  for (int p = 0; p < P; ++p) mx = fmaxf(mx, lg[p]);
+  float w[16];
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) {
+    w[p] = expf(lg[p] - mx);
+    s += w[p];
+  }
+  const float inv = 1.f / s;
+  for (int c4 = lane * 4; c4 < C; c4 += 256) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < P; ++p) {
+      const int64_t ip = (int64_t)item * P + p;
+      int x0, y0;
+      float wt[4];
+      bev_tap_geometry(pts, ip, Hv, Wv, inv_max_x, inv_max_y, x0, y0, wt);
+      float4 sp = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int yy = y0 + (t >> 1), xx = x0 + (t & 1);
+        if ((unsigned)yy < (unsigned)Hv && (unsigned)xx < (unsigned)Wv) {
+          const float4 v = *reinterpret_cast<const float4*>(vrows + (ip * 4 + t) * C + c4);
+          sp.x += v.x * wt[t];
+          sp.y += v.y * wt[t];
+          sp.z += v.z * wt[t];
+          sp.w += v.w * wt[t];
+        }
+      }
+      const float wp = w[p] * inv;
+      acc.x += wp * sp.x;
+      acc.y += wp * sp.y;
+      acc.z += wp * sp.z;
+      acc.w += wp * sp.w;
+    }
+    *reinterpret_cast<float4*>(out + (int64_t)item * C + c4) = acc;
+  }
+}
+
+void launch_bev_tap_rows(const float* pts, int* rows, int B, int Q, int P, int Hv, int Wv, float inv_max_x,
+                         float inv_max_y, hipStream_t st) {
+  const int64_t n = (int64_t)B * Q * P;
+  if (n == 0) return;
+  if ((int64_t)B * Hv * Wv >= (int64_t(1) << 31)) throw std::runtime_error("bev_tap_rows: map too large");
+  hipLaunchKernelGGL(bev_tap_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pts, rows, B, Q, P,
+                     Hv, Wv, inv_max_x, inv_max_y);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
+void launch_bev_sample_attn_gathered(const float* logits, const float* pts, const float* vrows, float* out, int B,
+                                     int Q, int P, int Hv, int Wv, int C, float inv_max_x, float inv_max_y,
+                                     hipStream_t st) {
+  if (P > 16 || C % 4) throw std::runtime_error("bev_sample_attn: P <= 16 and C % 4 == 0 required");
+  const int items = B * Q;
+  if (items == 0) return;
+  hipLaunchKernelGGL(bev_sample_attn_gathered_kernel, dim3((items + 3) / 4), dim3(256), 0, st, logits, pts, vrows,
+                     out, B, Q, P, Hv, Wv, C, inv_max_x, inv_max_y);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
 // ---------------------------------------------------------------- small MHA (nn.MultiheadAttention core)
 // One wave64 per (scene, head, query row): lanes own keys j and j+64 for the scores, softmax via
 // wave shuffles, then lanes (d, half) accumulate the P.V product over half the keys each.

@@ -125,7 +125,8 @@ bool launch_gemm_lat(const ConvArgs& a, hipStream_t st) {
   if (M64 == 0 || a.Cout == 0) return false;
   const int64_t tiles = ((M64 + kTM - 1) / kTM) * ((a.Cout + kTN - 1) / kTN);
   // small problems only: the tiled kernels win once there are thousands of tiles of work
-  if (M64 > 4160 || tiles > 2048) return false;
+  static const int64_t max_m = getenv("DDMI_GEMM_LAT_MAXM") ? atoll(getenv("DDMI_GEMM_LAT_MAXM")) : 4160;
+  if (M64 > max_m || tiles > 2048) return false;
   const dim3 grid((unsigned)((M64 + kTM - 1) / kTM), (unsigned)((a.Cout + kTN - 1) / kTN));
   hipLaunchKernelGGL(gemm_lat_kernel, grid, dim3(256), 0, st, a, (int)M64, K);
   DD_HIP_CHECK(hipGetLastError());

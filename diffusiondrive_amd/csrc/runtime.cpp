@@ -124,6 +124,8 @@ class Model {
   std::vector<hipEvent_t> fj_ev;
   size_t fj_next = 0;
   bool use_side = true;  // DDMI_STREAMS=0: everything on the main stream
+  // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
+  bool value_gather = true;
   // graph cache keyed by the forward's shape signature and the buffer generation
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
@@ -143,6 +145,7 @@ class Model {
     DD_HIP_CHECK(hipStreamCreateWithFlags(&st_side, hipStreamNonBlocking));
     st = st_main;
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -798,8 +801,12 @@ class Model {
     // on a third stream beside the first trajectory-head layer was measured: the graph put it on
     // the hardware queue of layer 0's and the head behind it - no overlap.)
     const int R = B * Q;  // trajectory query rows
-    float* vals[2];
-    for (int l = 0; l < 2; ++l) {
+    // In f16x3 mode the conv is instead evaluated per (step, layer) at the B x Q x P x 4 bilinear taps
+    // grid_sample reads (gathered rows, below): 40960 rows per call at B = 64 instead of 262144 per layer.
+    const bool gathered = value_gather && gemm_mode == DD_GEMM_F16X3 && dl[0].vproj.x3.hi != kNone &&
+                          dl[1].vproj.x3.hi != kNone;
+    float* vals[2] = {nullptr, nullptr};
+    for (int l = 0; l < 2 && !gathered; ++l) {
       vals[l] = buf("value_l" + std::to_string(l), (size_t)MB * d);
       conv_c(dl[l].vproj, cross, B, HB, WB, vals[l], true);
     }
@@ -903,9 +910,29 @@ class Model {
         // GridSampleCrossBEVAttention
         gemm(w.attw, tfe, d, R, logit, P);
         float* gso = buf("gs" + sfx, (size_t)R * d);
-        launch("bev_sample", 0, [&] {
-          launch_bev_sample_attn(logit, cur, vals[l], gso, B, Q, P, HB, WB, d, 1.0f / 32.0f, 1.0f / 32.0f, st);
-        });
+        if (gathered) {
+          const int MR = R * P * 4;
+          int* rows = reinterpret_cast<int*>(buf("value_taps" + sfx, (size_t)MR));
+          float* vrows = buf("value_rows" + sfx, (size_t)MR * d);
+          launch("misc", 0, [&] { launch_bev_tap_rows(cur, rows, B, Q, P, HB, WB, 1.0f / 32.0f, 1.0f / 32.0f, st); });
+          ConvArgs a = conv_args(w.vproj, cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, B, HB, WB, vrows,
+                                 (int64_t)MR * d, d, 0, true, nullptr, 0, 0, 0);
+          a.Nimg = 1;
+          a.Ho = MR;
+          a.Wo = 1;
+          a.rowmap = rows;
+          a.rowmap_nimg = B;
+          const double fl = 2.0 * MR * (double)d * 9 * w.vproj.cin_real;
+          launch("conv_x3", fl, [&] { launch_conv_gemm(a, st); }, &a);
+          launch("bev_sample", 0, [&] {
+            launch_bev_sample_attn_gathered(logit, cur, vrows, gso, B, Q, P, HB, WB, d, 1.0f / 32.0f, 1.0f / 32.0f,
+                                            st);
+          });
+        } else {
+          launch("bev_sample", 0, [&] {
+            launch_bev_sample_attn(logit, cur, vals[l], gso, B, Q, P, HB, WB, d, 1.0f / 32.0f, 1.0f / 32.0f, st);
+          });
+        }
         gemm(w.outp, gso, d, R, x1, d, false, tfe, d);
         // cross_agent_attention + norm1
         gemm(w.ag_q, x1, d, R, qa, d);

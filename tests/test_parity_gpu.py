@@ -70,8 +70,9 @@ def test_forward_matches_reference_goldens(gpu_model, path, mode):
     for s in range(2):
         for l in range(2):
             taps[f"gs_s{s}l{l}"] = gpu_model.tap(f"gs_s{s}l{l}", (B, 20, 256))
-    for l in range(2):
-        taps[f"value_call{l}_l{l}"] = _nchw(gpu_model.tap(f"value_l{l}"), B, 64, 64, 256)
+    if mode != "f16x3":  # f16x3 evaluates value_proj only at the sampled taps (test below)
+        for l in range(2):
+            taps[f"value_call{l}_l{l}"] = _nchw(gpu_model.tap(f"value_l{l}"), B, 64, 64, 256)
     tap_errs = {k: compare_tap(g, k, v.cpu().numpy()) for k, v in taps.items()}
     for k, v in errs.items():
         lines.append(f"  {k:22s} max abs err {v:.3e}")
@@ -182,3 +183,48 @@ def test_bf16_mode_is_reduced_precision_but_sane(gpu_model, seeded_sd):
     l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
     _report([f"== bf16 mode B=4: waypoint L2 vs fp32 oracle {l2:.3e} (reduced precision, not parity)"])
     assert np.isfinite(l2) and l2 < 1.0
+
+
+def test_gathered_value_rows_match_dense_map(gpu_model):
+    """f16x3 evaluates value_proj (blocks.py:68-76,114) only at the bilinear taps grid_sample reads
+    (conv_x3 gathered rows): every row must equal the fp32 dense map at its tap pixel, the tap
+    pixels must follow grid_sample's align_corners=False / zero-padding geometry (blocks.py:101-122),
+    and rows of zero-padded taps are -1. Checked on step 1 / layer 0, whose points are the ``pts``
+    buffer at the end of the forward; the dense map does not depend on the points."""
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B, Q, P, HB = 4, 20, 8, 64
+    inp = synthetic_inputs(B, 5)
+    # push some points off the 64 x 64 BEV map so zero-padded taps are exercised
+    nz = inp["noise"].copy()
+    nz[:, :3] *= 40.0
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    gpu_model.set_gemm_mode("fp32")
+    gpu_model.forward(feats, noise=torch.from_numpy(nz))
+    dense = gpu_model.tap("value_l0", (B, HB, HB, 256)).double().cpu().numpy().reshape(-1, 256)
+    gpu_model.set_gemm_mode("f16x3")
+    try:
+        gpu_model.forward(feats, noise=torch.from_numpy(nz))
+        n = B * Q * P * 4
+        rows = gpu_model.tap("value_taps_s1l0")[:n].view(torch.int32).cpu().numpy()
+        vals = gpu_model.tap("value_rows_s1l0", (n, 256)).double().cpu().numpy()
+        pts = gpu_model.tap("pts", (B * Q * P, 2)).double().cpu().numpy()
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    # tap geometry (float32 arithmetic as the kernel / F.grid_sample)
+    p32 = pts.astype(np.float32)
+    ix = ((p32[:, 1] / np.float32(32) + 1) * np.float32(HB) - 1) / 2
+    iy = ((p32[:, 0] / np.float32(32) + 1) * np.float32(HB) - 1) / 2
+    x0, y0 = np.floor(ix).astype(np.int64), np.floor(iy).astype(np.int64)
+    b = np.arange(B * Q * P) // (Q * P)
+    exp = []
+    for dy, dx in ((0, 0), (0, 1), (1, 0), (1, 1)):
+        yy, xx = y0 + dy, x0 + dx
+        ok = (yy >= 0) & (yy < HB) & (xx >= 0) & (xx < HB)
+        exp.append(np.where(ok, (b * HB + yy) * HB + xx, -1))
+    exp = np.stack(exp, 1).reshape(-1)
+    assert np.array_equal(rows, exp)
+    assert (rows < 0).any() and (rows >= 0).any()
+    ok = rows >= 0
+    ref = dense[rows[ok]]
+    err = np.abs(vals[ok] - ref).max() / max(1.0, np.abs(ref).max())
+    assert err <= TAP_TOL, err
