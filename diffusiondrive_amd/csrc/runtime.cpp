@@ -141,8 +141,21 @@ class Model {
     build(bx);
     ar.upload();
     decoder_init_constants();
-    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_main, hipStreamNonBlocking));
-    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_side, hipStreamNonBlocking));
+    // DDMI_SIDE_PRIO / DDMI_MAIN_PRIO = 1: that stream at the device's greatest priority. Measured
+    // (B = 64 bench graph): 4092 scenes/s default, 3950 side-high, 3968 main-high; both streams
+    // created explicitly at the LEAST priority dropped to 2725 - keep the default-priority streams.
+    int prio_least = 0, prio_greatest = 0;
+    DD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+    (void)prio_least;
+    auto make_stream = [&](hipStream_t* s, const char* env) {
+      const char* e = getenv(env);
+      if (e && atoi(e) != 0)
+        DD_HIP_CHECK(hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio_greatest));
+      else
+        DD_HIP_CHECK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+    };
+    make_stream(&st_main, "DDMI_MAIN_PRIO");
+    make_stream(&st_side, "DDMI_SIDE_PRIO");
     st = st_main;
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
@@ -668,6 +681,40 @@ class Model {
     float* ag_labels = nullptr;
   };
 
+  // denoise timesteps. truncated: roll_timesteps = round(arange(steps) * step_span / steps)[::-1]
+  // (:585-588; numpy round-half-even), DDIM prev = t - 1 (set_timesteps(1000), :584);
+  // vanilla: diffusers "leading" set_timesteps(steps): t_i = (steps-1-i) * (1000 / steps), prev = t - ratio.
+  std::vector<int> denoise_timesteps(int steps) const {
+    const bool vanilla = schedule == DD_SCHED_VANILLA;
+    std::vector<int> roll(steps);
+    const int ratio = vanilla ? 1000 / steps : 1;
+    for (int s = 0; s < steps; ++s)
+      roll[steps - 1 - s] = vanilla ? s * ratio
+                                    : (int)std::nearbyint((double)s * ((double)cfg.step_span / (double)steps));
+    return roll;
+  }
+  // time_mlp (SinusoidalPosEmb -> Linear -> Mish -> Linear, :463-468) -> Mish -> FiLM scale / shift
+  // of both decoder layers (:259-294), for every denoise step. Input-independent, so it runs on the
+  // side stream at the start of the forward, beside the LiDAR stem, off the trajectory head's path.
+  void time_film(int steps) {
+    const int d = 256;
+    const std::vector<int> roll = denoise_timesteps(steps);
+    float* te0 = buf("temb0", d);
+    float* te1 = buf("temb1", 4 * d);
+    float* te2 = buf("temb2", d);
+    float* mte = buf("temb_mish", d);
+    for (int si = 0; si < steps; ++si) {
+      const int k = roll[si];
+      launch("misc", 0, [&] { launch_timestep_embed((float)k, te0, d, st); });
+      gemm(tm1, te0, d, 1, te1, 4 * d);
+      launch("misc", 0, [&] { launch_activation(te1, te1, 4 * d, 0, st); });
+      gemm(tm3, te1, 4 * d, 1, te2, d);
+      launch("misc", 0, [&] { launch_activation(te2, mte, d, 0, st); });
+      for (int l = 0; l < 2; ++l)
+        gemm(dl[l].film, mte, d, 1, buf("film_s" + std::to_string(si) + "l" + std::to_string(l), 2 * d), 2 * d);
+    }
+  }
+
   void forward_body(int B, int steps, bool heads) {
     const int d = 256, Q = cfg.num_modes, P = cfg.num_poses;
     const int HC = cfg.cam_h, WC = cfg.cam_w, HL = cfg.lidar_h, WL = cfg.lidar_w;
@@ -688,6 +735,7 @@ class Model {
     float* pool_l = buf("lid_pool", (size_t)B * hl2 * wl2 * 64);
     fork();
     side([&] {
+      time_film(steps);
       stem_and_pool(lid.stem, lid4, B, HL, WL, stem_l, pool_l, hl2, wl2);
     });
     stem_and_pool(img.stem, cam4, B, HC, WC, stem_i, pool_i, hi2, wi2);
@@ -869,34 +917,41 @@ class Model {
     float* r1 = buf("dr1", (size_t)R * d);
     float* r2 = buf("dr2", (size_t)R * d);
     float* rr = buf("dr", (size_t)R * P * 3);
-    // truncated: roll_timesteps = round(arange(steps) * step_span / steps)[::-1] (:585-588; numpy
-    // round-half-even), DDIM prev = t - 1 (set_timesteps(1000), :584);
-    // vanilla: diffusers "leading" set_timesteps(steps): t_i = (steps-1-i) * (1000 / steps), prev = t - ratio.
-    std::vector<int> roll(steps);
+    const std::vector<int> roll = denoise_timesteps(steps);
     const int ratio = vanilla ? 1000 / steps : 1;
-    for (int s = 0; s < steps; ++s)
-      roll[steps - 1 - s] = vanilla ? s * ratio
-                                    : (int)std::nearbyint((double)s * ((double)cfg.step_span / (double)steps));
     float* reg_last = nullptr;
     float* cls_last = nullptr;
     for (int si = 0; si < steps; ++si) {
       const int k = roll[si];
-      // time embedding -> Mish -> FiLM scale / shift of both layers, on the side stream beside the
-      // trajectory embedding and the first layer's attention / FFN (joined before its norm3)
-      float* mte = buf("temb_mish", d);
+      // FiLM scale / shift of both layers: computed by time_film() at the start of the forward
       float* film_ss[2];
       for (int l = 0; l < 2; ++l)
         film_ss[l] = buf("film_s" + std::to_string(si) + "l" + std::to_string(l), 2 * d);
-      fork();
-      side([&] {
-        launch("misc", 0, [&] { launch_timestep_embed((float)k, te0, d, st); });
-        gemm(tm1, te0, d, 1, te1, 4 * d);
-        launch("misc", 0, [&] { launch_activation(te1, te1, 4 * d, 0, st); });
-        gemm(tm3, te1, 4 * d, 1, te2, d);
-        launch("misc", 0, [&] { launch_activation(te2, mte, d, 0, st); });
-        for (int l = 0; l < 2; ++l) gemm(dl[l].film, mte, d, 1, film_ss[l], 2 * d);
-      });
       launch("misc", 0, [&] { launch_traj_embed(imgx, pts, emb, R, P, st); });
+      // gathered value_proj of layer 0 (its points are known now) on the side stream, beside the
+      // trajectory-feature GEMMs; layer 1's follows layer 0's reg branch on the main stream
+      float* vrows_l[2] = {nullptr, nullptr};
+      auto gather_value = [&](int l, const float* pts_l) {
+        const std::string sfx = "_s" + std::to_string(si) + "l" + std::to_string(l);
+        const int MR = R * P * 4;
+        int* rows = reinterpret_cast<int*>(buf("value_taps" + sfx, (size_t)MR));
+        float* vrows = buf("value_rows" + sfx, (size_t)MR * d);
+        launch("misc", 0, [&] { launch_bev_tap_rows(pts_l, rows, B, Q, P, HB, WB, 1.0f / 32.0f, 1.0f / 32.0f, st); });
+        ConvArgs a = conv_args(dl[l].vproj, cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, B, HB, WB, vrows,
+                               (int64_t)MR * d, d, 0, true, nullptr, 0, 0, 0);
+        a.Nimg = 1;
+        a.Ho = MR;
+        a.Wo = 1;
+        a.rowmap = rows;
+        a.rowmap_nimg = B;
+        const double fl = 2.0 * MR * (double)d * 9 * dl[l].vproj.cin_real;
+        launch("conv_x3", fl, [&] { launch_conv_gemm(a, st); }, &a);
+        vrows_l[l] = vrows;
+      };
+      if (gathered) {
+        fork();
+        side([&] { gather_value(0, pts); });
+      }
       gemm(pa0, emb, 512, R, tf1, d, true);
       ln(pa2, tf1, d, tf1, d, R);
       gemm(pa3, tf1, d, R, tfe, d);
@@ -911,19 +966,11 @@ class Model {
         gemm(w.attw, tfe, d, R, logit, P);
         float* gso = buf("gs" + sfx, (size_t)R * d);
         if (gathered) {
-          const int MR = R * P * 4;
-          int* rows = reinterpret_cast<int*>(buf("value_taps" + sfx, (size_t)MR));
-          float* vrows = buf("value_rows" + sfx, (size_t)MR * d);
-          launch("misc", 0, [&] { launch_bev_tap_rows(cur, rows, B, Q, P, HB, WB, 1.0f / 32.0f, 1.0f / 32.0f, st); });
-          ConvArgs a = conv_args(w.vproj, cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, B, HB, WB, vrows,
-                                 (int64_t)MR * d, d, 0, true, nullptr, 0, 0, 0);
-          a.Nimg = 1;
-          a.Ho = MR;
-          a.Wo = 1;
-          a.rowmap = rows;
-          a.rowmap_nimg = B;
-          const double fl = 2.0 * MR * (double)d * 9 * w.vproj.cin_real;
-          launch("conv_x3", fl, [&] { launch_conv_gemm(a, st); }, &a);
+          if (l == 0)
+            join();  // layer 0's gathered value rows
+          else
+            gather_value(l, cur);
+          float* vrows = vrows_l[l];
           launch("bev_sample", 0, [&] {
             launch_bev_sample_attn_gathered(logit, cur, vrows, gso, B, Q, P, HB, WB, d, 1.0f / 32.0f, 1.0f / 32.0f,
                                             st);
@@ -947,7 +994,6 @@ class Model {
         // ffn -> norm3 -> FiLM time modulation
         gemm(w.ffn0, x3, d, R, hf, 1024, true);
         gemm(w.ffn2, hf, 1024, R, x2, d);
-        if (l == 0) join();  // FiLM scale / shift from the side stream
         ln(w.n3, x2, d, x2, d, R, nullptr, 0, 1, ss, ss + d);
         // task decoder: cls branch on the side stream beside the reg branch (and the next layer)
         float* cls = buf("cls" + sfx, R);
