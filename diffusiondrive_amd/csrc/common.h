@@ -137,9 +137,15 @@ void launch_bev_sample_attn(const float* logits, const float* pts, const float* 
 // attention over a compact (B*Q*P*4, C) value array holding the conv at those taps.
 void launch_bev_tap_rows(const float* pts, int* rows, int B, int Q, int P, int Hv, int Wv, float inv_max_x,
                          float inv_max_y, hipStream_t st);
-void launch_bev_sample_attn_gathered(const float* logits, const float* pts, const float* vrows, float* out, int B,
-                                     int Q, int P, int Hv, int Wv, int C, float inv_max_x, float inv_max_y,
-                                     hipStream_t st);
+// Deduplicated taps (one workgroup per scene, Hv * Wv <= 4096, else false and nothing launched):
+// rows[b * Q*P*4 + j] = the scene's j-th distinct tap pixel (pixel order; -1 past its count),
+// slots[tap] = the compact row holding the tap's pixel (-1 for zero padding).
+bool launch_bev_tap_dedup(const float* pts, int* rows, int* slots, int B, int Q, int P, int Hv, int Wv,
+                          float inv_max_x, float inv_max_y, hipStream_t st);
+// slots == nullptr: row of tap t of point ip is ip * 4 + t (launch_bev_tap_rows layout)
+void launch_bev_sample_attn_gathered(const float* logits, const float* pts, const float* vrows, const int* slots,
+                                     float* out, int B, int Q, int P, int Hv, int Wv, int C, float inv_max_x,
+                                     float inv_max_y, hipStream_t st);
 // Small multi-head attention: out[b,i,h*hd+d] = sum_j softmax_j(q.k / sqrt(hd)) v. Lk <= 128, hd <= 64.
 void launch_mha_small(const float* q, int64_t ldq, const float* k, const float* v, int64_t ldkv,
                       float* out, int64_t ldo, int B, int Lq, int Lk, int nh, int hd,

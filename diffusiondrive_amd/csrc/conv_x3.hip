@@ -102,6 +102,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   const int kq = tid & 7;  // float4 index inside the 32-wide K chunk
   int abase[A_LD], aih0[A_LD], aiw0[A_LD];
   uint32_t amask[A_LD];
+  int any_row = 0;  // gathered rows: some row of this tile is live
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = m0 + (tid >> 3) + (NT / 8) * i;
@@ -116,6 +117,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
       // gathered rows: the pixel comes from the row map (stride 1: output geometry = input's)
       const int px = v ? a.rowmap[m] : -1;
       rv = px >= 0;
+      any_row |= (int)rv;
       const int pp = rv ? px : 0;
       ow = pp % a.W;
       oh = (pp / a.W) % a.H;
@@ -137,6 +139,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
       aiw0[i] = iw0;
     }
   }
+  // gathered rows: a tile whose rows are all don't-care (-1: the unused tail of a scene's
+  // deduplicated pixel list) does no work; the predicate is workgroup-uniform
+  if (MODE == 1 && a.rowmap && !__syncthreads_or(any_row)) return;
   // B rows: constant part of the byte offset and validity
   uint32_t boff[B_LD];
   bool bok[B_LD];

@@ -208,9 +208,73 @@ __global__ __launch_bounds__(256) void bev_tap_rows_kernel(const float* __restri
   *reinterpret_cast<int4*>(rows + ip * 4) = r;
 }
 
+// Deduplicated form: one workgroup per scene marks the map pixels its Q x P x 4 taps read in an
+// LDS table, compacts them in pixel order into rows[b * cap .. b * cap + count) (the rest -1, so
+// the conv's tiles past a scene's count exit at once; cap = Q * P * 4 keeps scene blocks at fixed
+// offsets) and writes each tap's compact row (or -1 for a zero-padded tap) to slots.
+__global__ __launch_bounds__(256) void bev_tap_dedup_kernel(const float* __restrict__ pts, int* __restrict__ rows,
+                                                            int* __restrict__ slots, int Q, int P, int Hv, int Wv,
+                                                            float inv_max_x, float inv_max_y) {
+  __shared__ int table[4096];
+  __shared__ int scan[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int HW = Hv * Wv, QP = Q * P, cap = QP * 4;
+  const int64_t base = (int64_t)b * cap;
+  for (int e = tid; e < HW; e += 256) table[e] = 0;
+  __syncthreads();
+  for (int u = tid; u < QP; u += 256) {
+    int x0, y0;
+    float wt[4];
+    bev_tap_geometry(pts, (int64_t)b * QP + u, Hv, Wv, inv_max_x, inv_max_y, x0, y0, wt);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int yy = y0 + (t >> 1), xx = x0 + (t & 1);
+      if ((unsigned)yy < (unsigned)Hv && (unsigned)xx < (unsigned)Wv) table[yy * Wv + xx] = 1;
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the marks: thread t owns entries [t * E, t * E + E)
+  const int E = (HW + 255) / 256;
+  int cnt = 0;
+  for (int e = tid * E; e < min(HW, tid * E + E); ++e) cnt += table[e];
+  scan[tid] = cnt;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int v = tid >= off ? scan[tid - off] : 0;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  int r = scan[tid] - cnt;
+  const int total = scan[255];
+  for (int e = tid * E; e < min(HW, tid * E + E); ++e)
+    if (table[e]) {
+      table[e] = r;
+      rows[base + r] = b * HW + e;
+      ++r;
+    }
+  for (int j = total + tid; j < cap; j += 256) rows[base + j] = -1;
+  __syncthreads();
+  for (int u = tid; u < QP; u += 256) {
+    int x0, y0;
+    float wt[4];
+    bev_tap_geometry(pts, (int64_t)b * QP + u, Hv, Wv, inv_max_x, inv_max_y, x0, y0, wt);
+    int4 sl;
+    auto slot = [&](int yy, int xx) {
+      return ((unsigned)yy < (unsigned)Hv && (unsigned)xx < (unsigned)Wv) ? (int)(base + table[yy * Wv + xx]) : -1;
+    };
+    sl.x = slot(y0, x0);
+    sl.y = slot(y0, x0 + 1);
+    sl.z = slot(y0 + 1, x0);
+    sl.w = slot(y0 + 1, x0 + 1);
+    *reinterpret_cast<int4*>(slots + ((int64_t)b * QP + u) * 4) = sl;
+  }
+}
+
 __global__ __launch_bounds__(256) void bev_sample_attn_gathered_kernel(
     const float* __restrict__ logits, const float* __restrict__ pts, const float* __restrict__ vrows,
-    float* __restrict__ out, int B, int Q, int P, int Hv, int Wv, int C, float inv_max_x, float inv_max_y) {
+    const int* __restrict__ slots, float* __restrict__ out, int B, int Q, int P, int Hv, int Wv, int C,
+    float inv_max_x, float inv_max_y) {
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= B * Q) return;
@@ -236,7 +300,9 @@ __global__ __launch_bounds__(256) void bev_sample_attn_gathered_kernel(
       for (int t = 0; t < 4; ++t) {
         const int yy = y0 + (t >> 1), xx = x0 + (t & 1);
         if ((unsigned)yy < (unsigned)Hv && (unsigned)xx < (unsigned)Wv) {
-          const float4 v = *reinterpret_cast<const float4*>(vrows + (ip * 4 + t) * C + c4);
+          // compact row of this tap: its own (ip * 4 + t) without dedup, else the scene's pixel slot
+          const int64_t row = slots ? (int64_t)slots[ip * 4 + t] : ip * 4 + t;
+          const float4 v = *reinterpret_cast<const float4*>(vrows + row * C + c4);
           sp.x += v.x * wt[t];
           sp.y += v.y * wt[t];
           sp.z += v.z * wt[t];
@@ -263,14 +329,25 @@ void launch_bev_tap_rows(const float* pts, int* rows, int B, int Q, int P, int H
   DD_HIP_CHECK(hipGetLastError());
 }
 
-void launch_bev_sample_attn_gathered(const float* logits, const float* pts, const float* vrows, float* out, int B,
-                                     int Q, int P, int Hv, int Wv, int C, float inv_max_x, float inv_max_y,
-                                     hipStream_t st) {
+bool launch_bev_tap_dedup(const float* pts, int* rows, int* slots, int B, int Q, int P, int Hv, int Wv,
+                          float inv_max_x, float inv_max_y, hipStream_t st) {
+  if (Hv * Wv > 4096 || (int64_t)B * Q * P * 4 >= (int64_t(1) << 31) || (int64_t)B * Hv * Wv >= (int64_t(1) << 31))
+    return false;
+  if (B == 0) return true;
+  hipLaunchKernelGGL(bev_tap_dedup_kernel, dim3(B), dim3(256), 0, st, pts, rows, slots, Q, P, Hv, Wv, inv_max_x,
+                     inv_max_y);
+  DD_HIP_CHECK(hipGetLastError());
+  return true;
+}
+
+void launch_bev_sample_attn_gathered(const float* logits, const float* pts, const float* vrows, const int* slots,
+                                     float* out, int B, int Q, int P, int Hv, int Wv, int C, float inv_max_x,
+                                     float inv_max_y, hipStream_t st) {
   if (P > 16 || C % 4) throw std::runtime_error("bev_sample_attn: P <= 16 and C % 4 == 0 required");
   const int items = B * Q;
   if (items == 0) return;
   hipLaunchKernelGGL(bev_sample_attn_gathered_kernel, dim3((items + 3) / 4), dim3(256), 0, st, logits, pts, vrows,
-                     out, B, Q, P, Hv, Wv, C, inv_max_x, inv_max_y);
+                     slots, out, B, Q, P, Hv, Wv, C, inv_max_x, inv_max_y);
   DD_HIP_CHECK(hipGetLastError());
 }
 

@@ -126,6 +126,7 @@ class Model {
   bool use_side = true;  // DDMI_STREAMS=0: everything on the main stream
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
+  bool value_dedup = true;  // ... each distinct tap pixel of a scene once (DDMI_VALUE_DEDUP=0: every tap)
   // graph cache keyed by the forward's shape signature and the buffer generation
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
@@ -159,6 +160,7 @@ class Model {
     st = st_main;
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -931,12 +933,23 @@ class Model {
       // gathered value_proj of layer 0 (its points are known now) on the side stream, beside the
       // trajectory-feature GEMMs; layer 1's follows layer 0's reg branch on the main stream
       float* vrows_l[2] = {nullptr, nullptr};
+      const int* vslots_l[2] = {nullptr, nullptr};
       auto gather_value = [&](int l, const float* pts_l) {
         const std::string sfx = "_s" + std::to_string(si) + "l" + std::to_string(l);
         const int MR = R * P * 4;
         int* rows = reinterpret_cast<int*>(buf("value_taps" + sfx, (size_t)MR));
+        int* slots = value_dedup ? reinterpret_cast<int*>(buf("value_slots" + sfx, (size_t)MR)) : nullptr;
         float* vrows = buf("value_rows" + sfx, (size_t)MR * d);
-        launch("misc", 0, [&] { launch_bev_tap_rows(pts_l, rows, B, Q, P, HB, WB, 1.0f / 32.0f, 1.0f / 32.0f, st); });
+        bool dd = false;
+        if (slots)
+          launch("misc", 0, [&] {
+            dd = launch_bev_tap_dedup(pts_l, rows, slots, B, Q, P, HB, WB, 1.0f / 32.0f, 1.0f / 32.0f, st);
+          });
+        if (!dd) {
+          slots = nullptr;
+          launch("misc", 0, [&] { launch_bev_tap_rows(pts_l, rows, B, Q, P, HB, WB, 1.0f / 32.0f, 1.0f / 32.0f, st); });
+        }
+        vslots_l[l] = slots;
         ConvArgs a = conv_args(dl[l].vproj, cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, B, HB, WB, vrows,
                                (int64_t)MR * d, d, 0, true, nullptr, 0, 0, 0);
         a.Nimg = 1;
@@ -972,8 +985,8 @@ class Model {
             gather_value(l, cur);
           float* vrows = vrows_l[l];
           launch("bev_sample", 0, [&] {
-            launch_bev_sample_attn_gathered(logit, cur, vrows, gso, B, Q, P, HB, WB, d, 1.0f / 32.0f, 1.0f / 32.0f,
-                                            st);
+            launch_bev_sample_attn_gathered(logit, cur, vrows, vslots_l[l], gso, B, Q, P, HB, WB, d, 1.0f / 32.0f,
+                                            1.0f / 32.0f, st);
           });
         } else {
           launch("bev_sample", 0, [&] {

@@ -186,13 +186,16 @@ def test_bf16_mode_is_reduced_precision_but_sane(gpu_model, seeded_sd):
 
 
 def test_gathered_value_rows_match_dense_map(gpu_model):
-    """f16x3 evaluates value_proj (blocks.py:68-76,114) only at the bilinear taps grid_sample reads
-    (conv_x3 gathered rows): every row must equal the fp32 dense map at its tap pixel, the tap
-    pixels must follow grid_sample's align_corners=False / zero-padding geometry (blocks.py:101-122),
-    and rows of zero-padded taps are -1. Checked on step 1 / layer 0, whose points are the ``pts``
-    buffer at the end of the forward; the dense map does not depend on the points."""
+    """f16x3 evaluates value_proj (blocks.py:68-76,114) only at the map pixels grid_sample's bilinear
+    taps read (blocks.py:101-122), each distinct pixel of a scene once (conv_x3 gathered rows):
+    the tap geometry must follow align_corners=False / zero padding, each scene's row list must be
+    exactly its distinct tap pixels in pixel order (-1 past the count), every tap's slot must hold
+    its pixel (-1 for zero-padded taps), and every gathered row must equal the fp32 dense map at its
+    pixel. Checked on step 1 / layer 0, whose points are the ``pts`` buffer at the end of the
+    forward; the dense map does not depend on the points."""
     from diffusiondrive_amd.weights import synthetic_inputs
     B, Q, P, HB = 4, 20, 8, 64
+    cap = Q * P * 4
     inp = synthetic_inputs(B, 5)
     # push some points off the 64 x 64 BEV map so zero-padded taps are exercised
     nz = inp["noise"].copy()
@@ -204,8 +207,9 @@ def test_gathered_value_rows_match_dense_map(gpu_model):
     gpu_model.set_gemm_mode("f16x3")
     try:
         gpu_model.forward(feats, noise=torch.from_numpy(nz))
-        n = B * Q * P * 4
+        n = B * cap
         rows = gpu_model.tap("value_taps_s1l0")[:n].view(torch.int32).cpu().numpy()
+        slots = gpu_model.tap("value_slots_s1l0")[:n].view(torch.int32).cpu().numpy()
         vals = gpu_model.tap("value_rows_s1l0", (n, 256)).double().cpu().numpy()
         pts = gpu_model.tap("pts", (B * Q * P, 2)).double().cpu().numpy()
     finally:
@@ -216,15 +220,22 @@ def test_gathered_value_rows_match_dense_map(gpu_model):
     iy = ((p32[:, 0] / np.float32(32) + 1) * np.float32(HB) - 1) / 2
     x0, y0 = np.floor(ix).astype(np.int64), np.floor(iy).astype(np.int64)
     b = np.arange(B * Q * P) // (Q * P)
-    exp = []
+    pix = []
     for dy, dx in ((0, 0), (0, 1), (1, 0), (1, 1)):
         yy, xx = y0 + dy, x0 + dx
         ok = (yy >= 0) & (yy < HB) & (xx >= 0) & (xx < HB)
-        exp.append(np.where(ok, (b * HB + yy) * HB + xx, -1))
-    exp = np.stack(exp, 1).reshape(-1)
-    assert np.array_equal(rows, exp)
-    assert (rows < 0).any() and (rows >= 0).any()
-    ok = rows >= 0
-    ref = dense[rows[ok]]
-    err = np.abs(vals[ok] - ref).max() / max(1.0, np.abs(ref).max())
+        pix.append(np.where(ok, (b * HB + yy) * HB + xx, -1))
+    pix = np.stack(pix, 1).reshape(-1)
+    assert (pix < 0).any() and (pix >= 0).any()
+    for s_ in range(B):
+        tp = pix[s_ * cap:(s_ + 1) * cap]
+        uniq = np.unique(tp[tp >= 0])
+        rs = rows[s_ * cap:(s_ + 1) * cap]
+        assert np.array_equal(rs[:len(uniq)], uniq) and (rs[len(uniq):] == -1).all(), s_
+    assert np.array_equal(slots < 0, pix < 0)
+    live = slots >= 0
+    assert np.array_equal(rows[slots[live]], pix[live])
+    used = rows >= 0
+    ref = dense[rows[used]]
+    err = np.abs(vals[used] - ref).max() / max(1.0, np.abs(ref).max())
     assert err <= TAP_TOL, err
