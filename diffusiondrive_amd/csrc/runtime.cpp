@@ -860,7 +860,10 @@ class Model {
       vals[l] = buf("value_l" + std::to_string(l), (size_t)MB * d);
       conv_c(dl[l].vproj, cross, B, HB, WB, vals[l], true);
     }
-    join();
+    // the tf decoder branch is joined only where the trajectory head first reads its output (the
+    // agent cross-attention of step 0 / layer 0): the trajectory embedding, anchor encoder, BEV
+    // sampling (and its gathered value rows) of that layer run beside the tf decoder's tail
+    bool tf_pending = true;
     const float* agents = q + d;   // rows 1..30
 
     // ---- optional heads (off the waypoint path), on the side stream beside the trajectory head
@@ -962,8 +965,12 @@ class Model {
         vrows_l[l] = vrows;
       };
       if (gathered) {
-        fork();
-        side([&] { gather_value(0, pts); });
+        if (si == 0) {
+          gather_value(0, pts);  // the side stream still carries the tf decoder
+        } else {
+          fork();
+          side([&] { gather_value(0, pts); });
+        }
       }
       gemm(pa0, emb, 512, R, tf1, d, true);
       ln(pa2, tf1, d, tf1, d, R);
@@ -979,10 +986,11 @@ class Model {
         gemm(w.attw, tfe, d, R, logit, P);
         float* gso = buf("gs" + sfx, (size_t)R * d);
         if (gathered) {
-          if (l == 0)
-            join();  // layer 0's gathered value rows
-          else
+          if (l == 0) {
+            if (si > 0) join();  // layer 0's gathered value rows
+          } else {
             gather_value(l, cur);
+          }
           float* vrows = vrows_l[l];
           launch("bev_sample", 0, [&] {
             launch_bev_sample_attn_gathered(logit, cur, vrows, vslots_l[l], gso, B, Q, P, HB, WB, d, 1.0f / 32.0f,
@@ -996,6 +1004,10 @@ class Model {
         gemm(w.outp, gso, d, R, x1, d, false, tfe, d);
         // cross_agent_attention + norm1
         gemm(w.ag_q, x1, d, R, qa, d);
+        if (tf_pending) {
+          join();  // tf decoder: agent K / V and ego rows of both layers
+          tf_pending = false;
+        }
         launch("mha", 0, [&] {
           launch_mha_small(qa, d, akv[l], akv[l] + d, 2 * d, gs, d, B, Q, 30, 8, 32, (int64_t)Q * d,
                            (int64_t)30 * 2 * d, (int64_t)Q * d, st);
