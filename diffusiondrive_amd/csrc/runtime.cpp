@@ -126,7 +126,9 @@ class Model {
   bool use_side = true;  // DDMI_STREAMS=0: everything on the main stream
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
-  bool value_dedup = true;  // ... each distinct tap pixel of a scene once (DDMI_VALUE_DEDUP=0: every tap)
+  bool value_dedup = true;
+  // bev_proj's keyval half at 8 x 8 before the upsample (DDMI_BEVPROJ_LOWRES=0: concat at 64 x 64)
+  bool bevproj_lowres = true;  // ... each distinct tap pixel of a scene once (DDMI_VALUE_DEDUP=0: every tap)
   // graph cache keyed by the forward's shape signature and the buffer generation
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
@@ -161,6 +163,7 @@ class Model {
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_BEVPROJ_LOWRES")) bevproj_lowres = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -580,6 +583,44 @@ class Model {
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
 
+  // C = A[:, 0:kn] W[:, k0:k0+kn]^T (+bias when with_bias) (+res) (relu): a K-slice of a Linear (the weight
+  // rows keep their full stride; 16-B aligned slices only)
+  void gemm_slice(const Lin& L, int k0, int kn, bool with_bias, const float* A, int64_t a_gs, int64_t a_rs, int G,
+                  int R, float* C, int64_t c_gs, int64_t c_rs, bool relu, const float* res, int64_t r_gs,
+                  int64_t r_rs) {
+    if (k0 % 8 || kn % 8 || k0 + kn > L.nin) throw std::runtime_error("gemm_slice: bad K slice");
+    ConvArgs a;
+    a.in = A;
+    a.in_sn = a_gs;
+    a.in_sh = a_rs;
+    a.in_sw = 0;
+    a.H = R;
+    a.W = 1;
+    a.Cin = kn;
+    a.wgt = W(L.w) + k0;
+    a.ldb = L.nin;
+    a.bias = with_bias ? W(L.b) : nullptr;
+    a.res = res;
+    a.res_sn = r_gs;
+    a.res_sh = r_rs;
+    a.out = C;
+    a.out_sn = c_gs;
+    a.out_sh = c_rs;
+    a.out_sw = 0;
+    a.Nimg = G;
+    a.Ho = R;
+    a.Wo = 1;
+    a.Cout = L.nout;
+    a.relu = relu;
+    use_split(a, L.x3);
+    if (a.wh) {
+      a.wh += k0;
+      if (L.x3.lo != kNone) a.wl += k0;
+    }
+    const double fl = 2.0 * G * R * (double)L.nout * kn;
+    launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
+  }
+
   void ln(const LNp& p, const float* x, int64_t ldx, float* y, int64_t ldy, int rows, const float* res = nullptr,
           int64_t ldres = 0, int res_div = 1, const float* fs = nullptr, const float* fb = nullptr) {
     launch("layernorm", 0, [&] {
@@ -836,15 +877,26 @@ class Model {
     conv(up4, up3, (int64_t)HB * WB * bc, (int64_t)WB * bc, bc, B, HB, WB, cross_in + 256, (int64_t)HB * WB * CC,
          (int64_t)WB * CC, CC, true);
 
-    // concat_cross_bev: keyval[:, :64] as (B,8,8,256) -> bilinear 64x64 -> channels 0..255
-    {
+    const int MB = B * HB * WB;
+    float* cross = buf("cross_bev", (size_t)MB * d);
+    if (bevproj_lowres) {
+      // bev_proj(cat(bilinear(keyval 8x8), p3)) = bilinear(W[:, :256] keyval) + W[:, 256:] p3 + b: bilinear
+      // interpolation is linear with weights summing to 1, so the keyval half of the 320 -> 256 projection runs
+      // on the 8 x 8 tokens and is upsampled into cross_bev, which the p3 half (K = 64) then adds to in place
+      float* kvp = buf("kv_proj", (size_t)B * 64 * d);
+      gemm_slice(bevproj, 0, d, false, KV, (int64_t)65 * d, d, B, 64, kvp, (int64_t)64 * d, d, false, nullptr, 0, 0);
+      View4 a{kvp, (int64_t)64 * d, (int64_t)8 * d, d, 1};
+      View4 o{cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, 1};
+      launch("bilinear", 0, [&] { launch_bilinear(a, B, 8, 8, d, o, HB, WB, 8.0f / HB, 8.0f / WB, 0, st); });
+      gemm_slice(bevproj, d, CC - d, true, cross_in + d, (int64_t)MB * CC, CC, 1, MB, cross, (int64_t)MB * d, d, true,
+                 cross, (int64_t)MB * d, d);
+    } else {
+      // concat_cross_bev: keyval[:, :64] as (B,8,8,256) -> bilinear 64x64 -> channels 0..255
       View4 a{KV, (int64_t)65 * d, (int64_t)8 * d, d, 1};
       View4 o{cross_in, (int64_t)HB * WB * CC, (int64_t)WB * CC, CC, 1};
       launch("bilinear", 0, [&] { launch_bilinear(a, B, 8, 8, d, o, HB, WB, 8.0f / HB, 8.0f / WB, 0, st); });
+      gemm(bevproj, cross_in, CC, MB, cross, d, true);
     }
-    const int MB = B * HB * WB;
-    float* cross = buf("cross_bev", (size_t)MB * d);
-    gemm(bevproj, cross_in, CC, MB, cross, d, true);
     ln(bevproj_ln, cross, d, cross, d, MB);
 
     // value_proj for both decoder layers (main stream, beside the tf decoder), then join. (Layer 1's
