@@ -585,7 +585,15 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   static const int use_x6 = getenv("DDMI_X6") ? atoi(getenv("DDMI_X6")) : 1;
   if (a.rowmap) {
     g_last_conv = "conv_x3";
-    launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);  // 128 x 128
+    static const int gt = getenv("DDMI_GATHER_TILE") ? atoi(getenv("DDMI_GATHER_TILE")) : 0;
+    if (gt == 1)
+      launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
+    else if (gt == 2)
+      launch_x3_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64
+    else if (gt == 3)
+      launch_x3_cfg<2, 2, 1, 2>(a, M, K, st);  // 64 x 128
+    else
+      launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);  // 128 x 128
     return;
   }
   if (use_x6 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x6(a, st)) {

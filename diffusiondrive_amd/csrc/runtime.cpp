@@ -916,6 +916,11 @@ class Model {
     // agent cross-attention of step 0 / layer 0): the trajectory embedding, anchor encoder, BEV
     // sampling (and its gathered value rows) of that layer run beside the tf decoder's tail
     bool tf_pending = true;
+    static const bool join_early = getenv("DDMI_TF_JOIN_EARLY") && atoi(getenv("DDMI_TF_JOIN_EARLY")) != 0;
+    if (join_early) {
+      join();
+      tf_pending = false;
+    }
     const float* agents = q + d;   // rows 1..30
 
     // ---- optional heads (off the waypoint path), on the side stream beside the trajectory head
