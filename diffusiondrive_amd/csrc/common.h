@@ -152,6 +152,11 @@ void launch_mha_small(const float* q, int64_t ldq, const float* k, const float* 
                       int64_t q_bstride, int64_t kv_bstride, int64_t o_bstride, hipStream_t st);
 // reg (rows, P, 3) from the raw branch output r (rows, P*3): xy += pts, heading = tanh * pi;
 // optionally also writes the cascade's next points (rows, P, 2).
+// Fused reg branch (Linear nin->nhid, ReLU, Linear nhid->nhid, ReLU, Linear nhid->nout) + the finalize below, fp32
+// VALU; false (nothing launched) unless nin = nhid = 256 and nout = P * 3 <= 32 (decoder.hip).
+bool launch_reg_mlp(const float* x, int64_t ldx, const float* w0, const float* b0, const float* w2, const float* b2,
+                    const float* w4, const float* b4, int nin, int nhid, int nout, const float* pts, float* reg,
+                    float* pts_next, int rows, int P, hipStream_t st);
 void launch_reg_finalize(const float* r, const float* pts, float* reg, float* pts_next, int rows, int P,
                          hipStream_t st);
 // img = DDIM.step(norm_odo(reg[..., :2]), t -> t-1, img), eta = 0, prediction 'sample', clip.

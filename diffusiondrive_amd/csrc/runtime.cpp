@@ -59,6 +59,8 @@ struct DiffLayerW {
   LNp n1, n2, n3;
   Lin c0, c3, c6, r0, r2, r4;
   LNp c2, c5;
+  // reg-branch weights k-blocked for the fused VALU kernel: [nin / 4][nout][4] (launch_reg_mlp)
+  size_t r0_kb = kNone, r2_kb = kNone, r4_kb = kNone;
 };
 
 struct KStat {
@@ -128,7 +130,11 @@ class Model {
   bool value_gather = true;
   bool value_dedup = true;
   // bev_proj's keyval half at 8 x 8 before the upsample (DDMI_BEVPROJ_LOWRES=0: concat at 64 x 64)
-  bool bevproj_lowres = true;  // ... each distinct tap pixel of a scene once (DDMI_VALUE_DEDUP=0: every tap)
+  bool bevproj_lowres = true;
+  // reg branch + finalize as one VALU kernel (DDMI_REG_FUSED=1). Off: measured in the B = 64 graph it takes
+  // ~31 us per layer against ~43 us for the three GEMMs + finalize, but the wall did not move (4150/4159 vs
+  // 4158/4189 scenes/s, same box) - the per-layer serial chain is bound by the k4 load latency it exposes
+  bool reg_fused = false;  // ... each distinct tap pixel of a scene once (DDMI_VALUE_DEDUP=0: every tap)
   // graph cache keyed by the forward's shape signature and the buffer generation
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
@@ -164,6 +170,7 @@ class Model {
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BEVPROJ_LOWRES")) bevproj_lowres = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_REG_FUSED")) reg_fused = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -267,6 +274,18 @@ class Model {
     return l;
   }
 
+  // W [nout][nin] -> [nin / 4][nout][4]: output j's 4 consecutive k at (k4 * nout + j) * 4, so a wave whose
+  // lanes are consecutive outputs reads 16 B per lane from one contiguous 1 KB segment
+  size_t prep_kblocked(const BlobIndex& bx, const std::string& name, int nout, int nin) {
+    if (nin % 4) throw std::runtime_error("prep_kblocked: nin % 4 != 0 for " + name);
+    const HostTensor& w = bx.get(name, {nout, nin});
+    std::vector<float> t((size_t)nout * nin);
+    for (int k4 = 0; k4 < nin / 4; ++k4)
+      for (int j = 0; j < nout; ++j)
+        for (int c = 0; c < 4; ++c) t[((size_t)k4 * nout + j) * 4 + c] = w.data[(size_t)j * nin + 4 * k4 + c];
+    return ar.add(t);
+  }
+
   void build(const BlobIndex& bx) {
     if (cfg.lidar_channels < 1 || cfg.lidar_channels > 4) throw std::invalid_argument("lidar_channels must be 1..4");
     build_trunk(bx, "_backbone.image_encoder", cfg.image_arch, 3, img);
@@ -362,6 +381,9 @@ class Model {
       w.r0 = prep_linear(bx, ar, t + ".plan_reg_branch.0", d, d);
       w.r2 = prep_linear(bx, ar, t + ".plan_reg_branch.2", d, d);
       w.r4 = prep_linear(bx, ar, t + ".plan_reg_branch.4", P * 3, d);
+      w.r0_kb = prep_kblocked(bx, t + ".plan_reg_branch.0.weight", d, d);
+      w.r2_kb = prep_kblocked(bx, t + ".plan_reg_branch.2.weight", d, d);
+      w.r4_kb = prep_kblocked(bx, t + ".plan_reg_branch.4.weight", P * 3, d);
       dl.push_back(w);
     }
     bevproj = prep_linear(bx, ar, "bev_proj.0", d, 320);
@@ -1087,12 +1109,23 @@ class Model {
           ln(w.c5, c2, d, c2, d, R);
           gemm(w.c6, c2, d, R, cls, 1);
         });
-        gemm(w.r0, x2, d, R, r1, d, true);
-        gemm(w.r2, r1, d, R, r2, d, true);
-        gemm(w.r4, r2, d, R, rr, P * 3);
         float* reg = buf("reg" + sfx, (size_t)R * P * 3);
         float* nxt = (l == 0) ? pts2 : nullptr;
-        launch("misc", 0, [&] { launch_reg_finalize(rr, cur, reg, nxt, R, P, st); });
+        bool fused = false;
+        if (reg_fused) {
+          const double fl = 2.0 * R * ((double)w.r0.nout * w.r0.nin + (double)w.r2.nout * w.r2.nin +
+                                       (double)w.r4.nout * w.r4.nin);
+          launch("misc", fl, [&] {
+            fused = launch_reg_mlp(x2, d, W(w.r0_kb), W(w.r0.b), W(w.r2_kb), W(w.r2.b), W(w.r4_kb), W(w.r4.b), w.r0.nin,
+                                   w.r0.nout, w.r4.nout, cur, reg, nxt, R, P, st);
+          });
+        }
+        if (!fused) {
+          gemm(w.r0, x2, d, R, r1, d, true);
+          gemm(w.r2, r1, d, R, r2, d, true);
+          gemm(w.r4, r2, d, R, rr, P * 3);
+          launch("misc", 0, [&] { launch_reg_finalize(rr, cur, reg, nxt, R, P, st); });
+        }
         cur = pts2;
         reg_last = reg;
         cls_last = cls;
