@@ -239,3 +239,30 @@ def test_gathered_value_rows_match_dense_map(gpu_model):
     ref = dense[rows[used]]
     err = np.abs(vals[used] - ref).max() / max(1.0, np.abs(ref).max())
     assert err <= TAP_TOL, err
+
+
+def test_fused_reg_branch_matches_gemm_path(gpu_model, seeded_sd, monkeypatch):
+    """DDMI_REG_FUSED=1 (reg branch Linear-ReLU-Linear-ReLU-Linear + finalize, transfuser_model_v2.py:208-256,
+    375-382, as one VALU kernel over k-blocked fp32 weights) against the default GEMM path on the same
+    inputs: every per-(step, layer) reg output within the 1e-4 bar."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 4
+    inp = synthetic_inputs(B, 17)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"])
+    gpu_model.set_gemm_mode("f16x3")
+    try:
+        ref_out = gpu_model.forward(feats, noise=nz)["trajectory"].numpy()
+        ref = {f"reg_s{s}l{l}": gpu_model.tap(f"reg_s{s}l{l}", (B, 20, 8, 3)).cpu().numpy()
+               for s in range(2) for l in range(2)}
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    monkeypatch.setenv("DDMI_REG_FUSED", "1")
+    monkeypatch.setenv("DDMI_GEMM", "f16x3")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0)
+    out = m.forward(feats, noise=nz)["trajectory"].numpy()
+    for k, v in ref.items():
+        got = m.tap(k, (B, 20, 8, 3)).cpu().numpy()
+        assert np.abs(got - v).max() <= 1e-4 * (1 + np.abs(v).max()), (k, np.abs(got - v).max())
+    assert np.abs(out - ref_out).max() <= 1e-3
