@@ -93,6 +93,12 @@ void launch_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow,
 // out[n,y,x,c] (= or +=) bilinear(in)[n,y,x,c]. ratio_h/ratio_w = in/out unless a scale factor is given.
 void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float ratio_h,
                      float ratio_w, int accumulate, hipStream_t st);
+// cross_bev = LN(ReLU(W p3 + bias + bilinear(kvp))) in one pass (elementwise.hip): p3 (B, H, 64, 64) strided,
+// kvp (B, Hk, Wk, 256) contiguous, w = the p3 columns of the projection (row stride ldw), out (B, H, 64, 256).
+// False (nothing launched) outside C = 256, 64 p3 channels, W = 64, Wk <= 8.
+bool launch_bevproj_fused(const float* p3, int64_t p3_sn, int64_t p3_sh, int64_t p3_sw, int Kp3, const float* kvp,
+                          int Hk, int Wk, const float* w, int ldw, const float* bias, const float* g, const float* be,
+                          float* out, int B, int H, int W, int C, hipStream_t st);
 // Row LayerNorm (eps 1e-5): y[r] = LN(x[r] + res[r / res_div]) * g + b, then optional FiLM
 // y = y * (1 + film_scale) + film_shift. C <= 2048. In-place allowed (y == x).
 void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldres, int res_div,

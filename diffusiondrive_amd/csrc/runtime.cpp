@@ -131,6 +131,10 @@ class Model {
   bool value_dedup = true;
   // bev_proj's keyval half at 8 x 8 before the upsample (DDMI_BEVPROJ_LOWRES=0: concat at 64 x 64)
   bool bevproj_lowres = true;
+  // ... and its p3 half + upsample + ReLU + LN as one VALU pass (DDMI_BEVPROJ_FUSED=1). Off: parity green, but
+  // the first form takes ~0.33 ms, the same as the upsample + K = 64 GEMM + LN it replaces (4186/4169 vs
+  // 4254/4148 scenes/s, same box)
+  bool bevproj_fused = false;
   // reg branch + finalize as one VALU kernel (DDMI_REG_FUSED=1). Off: measured in the B = 64 graph it takes
   // ~31 us per layer against ~43 us for the three GEMMs + finalize, but the wall did not move (4150/4159 vs
   // 4158/4189 scenes/s, same box) - the per-layer serial chain is bound by the k4 load latency it exposes
@@ -170,6 +174,7 @@ class Model {
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BEVPROJ_LOWRES")) bevproj_lowres = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_BEVPROJ_FUSED")) bevproj_fused = atoi(e) != 0;
     if (const char* e = getenv("DDMI_REG_FUSED")) reg_fused = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
@@ -907,19 +912,29 @@ class Model {
       // on the 8 x 8 tokens and is upsampled into cross_bev, which the p3 half (K = 64) then adds to in place
       float* kvp = buf("kv_proj", (size_t)B * 64 * d);
       gemm_slice(bevproj, 0, d, false, KV, (int64_t)65 * d, d, B, 64, kvp, (int64_t)64 * d, d, false, nullptr, 0, 0);
-      View4 a{kvp, (int64_t)64 * d, (int64_t)8 * d, d, 1};
-      View4 o{cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, 1};
-      launch("bilinear", 0, [&] { launch_bilinear(a, B, 8, 8, d, o, HB, WB, 8.0f / HB, 8.0f / WB, 0, st); });
-      gemm_slice(bevproj, d, CC - d, true, cross_in + d, (int64_t)MB * CC, CC, 1, MB, cross, (int64_t)MB * d, d, true,
-                 cross, (int64_t)MB * d, d);
+      bool fused = false;
+      if (bevproj_fused)  // p3 half + upsample + ReLU + LN in one VALU pass
+        launch("layernorm", 2.0 * MB * d * (CC - d), [&] {
+          fused = launch_bevproj_fused(cross_in + d, (int64_t)HB * WB * CC, (int64_t)WB * CC, CC, CC - d, kvp, 8, 8,
+                                       W(bevproj.w) + d, CC, W(bevproj.b), W(bevproj_ln.g), W(bevproj_ln.b), cross, B,
+                                       HB, WB, d, st);
+        });
+      if (!fused) {
+        View4 a{kvp, (int64_t)64 * d, (int64_t)8 * d, d, 1};
+        View4 o{cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, 1};
+        launch("bilinear", 0, [&] { launch_bilinear(a, B, 8, 8, d, o, HB, WB, 8.0f / HB, 8.0f / WB, 0, st); });
+        gemm_slice(bevproj, d, CC - d, true, cross_in + d, (int64_t)MB * CC, CC, 1, MB, cross, (int64_t)MB * d, d,
+                   true, cross, (int64_t)MB * d, d);
+        ln(bevproj_ln, cross, d, cross, d, MB);
+      }
     } else {
       // concat_cross_bev: keyval[:, :64] as (B,8,8,256) -> bilinear 64x64 -> channels 0..255
       View4 a{KV, (int64_t)65 * d, (int64_t)8 * d, d, 1};
       View4 o{cross_in, (int64_t)HB * WB * CC, (int64_t)WB * CC, CC, 1};
       launch("bilinear", 0, [&] { launch_bilinear(a, B, 8, 8, d, o, HB, WB, 8.0f / HB, 8.0f / WB, 0, st); });
       gemm(bevproj, cross_in, CC, MB, cross, d, true);
+      ln(bevproj_ln, cross, d, cross, d, MB);
     }
-    ln(bevproj_ln, cross, d, cross, d, MB);
 
     // value_proj for both decoder layers (main stream, beside the tf decoder), then join. (Layer 1's
     // on a third stream beside the first trajectory-head layer was measured: the graph put it on
