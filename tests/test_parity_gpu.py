@@ -266,3 +266,28 @@ def test_fused_reg_branch_matches_gemm_path(gpu_model, seeded_sd, monkeypatch):
         got = m.tap(k, (B, 20, 8, 3)).cpu().numpy()
         assert np.abs(got - v).max() <= 1e-4 * (1 + np.abs(v).max()), (k, np.abs(got - v).max())
     assert np.abs(out - ref_out).max() <= 1e-3
+
+
+def test_fused_bevproj_matches_default_path(gpu_model, seeded_sd, monkeypatch):
+    """DDMI_BEVPROJ_FUSED=1 (bev_proj's p3 half + bilinear upsample of the 8x8 keyval projection + ReLU +
+    LayerNorm in one VALU pass, transfuser_model_v2.py:123-140) against the default path: cross_bev and
+    the trajectories on the same inputs."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 2
+    inp = synthetic_inputs(B, 23)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"])
+    gpu_model.set_gemm_mode("f16x3")
+    try:
+        ref_out = gpu_model.forward(feats, noise=nz)["trajectory"].numpy()
+        ref = gpu_model.tap("cross_bev", (B, 4096, 256)).double().cpu().numpy()
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    monkeypatch.setenv("DDMI_BEVPROJ_FUSED", "1")
+    monkeypatch.setenv("DDMI_GEMM", "f16x3")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0)
+    out = m.forward(feats, noise=nz)["trajectory"].numpy()
+    got = m.tap("cross_bev", (B, 4096, 256)).double().cpu().numpy()
+    assert np.abs(got - ref).max() <= TAP_TOL * max(1.0, np.abs(ref).max())
+    assert np.abs(out - ref_out).max() <= 1e-3
