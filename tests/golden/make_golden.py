@@ -15,8 +15,10 @@ Noise is the reference's own draw: ``torch.manual_seed(seed)`` right before ``fo
 (transfuser_model_v2.py:593 is the only RNG consumer). Inputs are regenerated from the seed
 by ``synthetic_inputs`` and their checksums are stored so tests can confirm regeneration.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
-Writes tests/golden/ref_b{B}_s{seed}.npz and tests/golden/state_dict_schema.json.
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [B:seed ...]
+Writes tests/golden/ref_b{B}_s{seed}.npz and tests/golden/state_dict_schema.json. Default cases:
+B=1 (seed 11), B=4 (seed 1234) and B=64 (seed 1234) -- the last is exactly bench.py's rank-0
+workload (``synthetic_inputs(64, 1234)``), so the benchmark batch itself is pinned.
 Nothing of the reference's source is copied; only data (inputs/outputs) is stored.
 """
 import json
@@ -37,7 +39,7 @@ import torch  # noqa: E402
 from diffusiondrive_amd.config import TransfuserConfig  # noqa: E402
 from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs  # noqa: E402
 
-CASES = [(1, 11), (4, 1234)]
+CASES = [(1, 11), (4, 1234), (64, 1234)]
 WEIGHT_SEED = 0
 MAX_SAMPLES = 4096
 
@@ -73,7 +75,8 @@ def main():
     model.eval()
     torch.set_num_threads(8)
 
-    for B, seed in CASES:
+    cases = [tuple(int(x) for x in a.split(":")) for a in sys.argv[1:]] or CASES
+    for B, seed in cases:
         inp = synthetic_inputs(B, seed, cfg)
         cap = {}
         calls = {"layer": 0, "vp": 0, "gs": 0}
