@@ -4,23 +4,38 @@ steps) on MI355X, scenes/s at batch 64 per GPU (BASELINE.json metric / configs[1
 over 1/2/4/8 GPUs with one RCCL all_gather of the predicted trajectories per step).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+With ``--gpus N > 1`` and no ``$WORLD_SIZE`` the script launches N rank processes itself
+(torchrun-style: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their
+environment, nothing touches the GPU before that) and exits with the worst rank's code. Under
+``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` each rank reads the
+launcher's environment; a ``--gpus`` that disagrees with ``$WORLD_SIZE`` is an error.
 
 A step = one forward of B synthetic scenes resident in HBM (+ the all_gather when N > 1).
-Rank 0 prints ONE JSON line. Also reported:
-  * roofline: the dominant kernel (the conv / GEMM kernel with the most device time in the
-    profiled replay: conv_x6 for the default f16x3 path, conv_gemm for --gemm fp32), algorithmic
-    FLOP per launch / average launch time from HIP events recorded on the kernel's stream during a
-    profiled replay of the timed workload; peak = the algorithmic fp32 ceiling of the gemm mode
-    (157.3 TFLOP/s fp32 MFMA dense, or 2500 / 3 TFLOP/s for the 3-product f16 split,
-    MI355X_MICROARCH.md).
-  * cpu_baseline: the golden-pinned CPU oracle (oracle/, PyTorch-CPU fp32) timed on this host
-    on a bounded sample of the same workload (rank 0, N = 1 only); its outputs double as the
-    waypoint-L2 parity check of the GPU result on those scenes.
+Rank 0 prints ONE JSON line. Besides the contract fields it reports:
+  * ``median_ms_per_step``: median of the per-step HIP-event durations of the timed loop;
+  * ``fp32_leg``: the same workload on the fp32-MFMA path (N = 1), the conservative headline;
+  * ``h2d_included``: the same forward with its inputs copied from pinned host memory every
+    step (PCIe-inclusive; never ``value``);
+  * ``roofline``: the dominant kernel (the conv / GEMM kernel with the most device time in a
+    profiled single-stream replay: conv_x6 for the default f16x3 path), algorithmic FLOP per
+    launch / average launch time from HIP events recorded on the kernel's stream; peak = the
+    algorithmic fp32 ceiling of the gemm mode (157.3 TFLOP/s fp32 MFMA dense, or 2500 / 3
+    TFLOP/s for the 3-product f16 split, MI355X_MICROARCH.md); ``traffic`` = HBM bytes per
+    launch from the committed rocprofv3 PMC summary (FETCH x2 + WRITE, separate passes);
+  * ``whole_forward``: canonical GFLOP/scene AND the FLOPs the graph executes
+    (gathered value_proj, low-res bev_proj: fewer than canonical);
+  * ``cpu_baseline``: the golden-pinned CPU oracle (oracle/, PyTorch-CPU fp32) timed on this
+    host at 8 and 16 threads (the box's CPU share) on B = 64 and B = 1 samples of the same
+    workload (rank 0, N = 1 only); its outputs are the waypoint-L2 parity check of both GPU legs.
+``--cpu-plumbing`` (tests only) runs the launcher / gloo all_gather / max-over-ranks / JSON path
+on CPU with a stand-in step (zeros; no forward) so the multi-rank plumbing is testable here.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,22 +45,24 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+METRIC = "scenes/s at batch 64, 2 denoise steps, 1/2/4/8 MI355X; waypoint L2 vs ref"
 CANONICAL_GFLOP_PER_SCENE_2STEP = 65.27  # SURVEY.md §8d (value_proj once per layer)
 FP32_MFMA_PEAK_TFLOPS = 157.3            # MI355X dense fp32 MFMA (= vector) peak
-F16_MFMA_PEAK_TFLOPS = 2500.0            # MI355X dense f16 MFMA peak (no sparsity)
-# peak of ALGORITHMIC fp32 FLOPs per gemm mode: f16x3 issues 3 f16 MFMA products per fp32 MAC
-ALGO_PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16x3": F16_MFMA_PEAK_TFLOPS / 3}
+F16_MFMA_PEAK_TFLOPS = 2500.0            # MI355X dense f16 / bf16 MFMA peak (no sparsity)
+# peak of ALGORITHMIC FLOPs per gemm mode: f16x3 issues 3 f16 MFMA products per fp32 MAC
+ALGO_PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16x3": F16_MFMA_PEAK_TFLOPS / 3, "bf16": F16_MFMA_PEAK_TFLOPS}
 KERNEL_DESC = {
     "conv_gemm": "conv_gemm (implicit-GEMM conv / GEMM, fp32 MFMA v_mfma_f32_32x32x2_f32)",
     "conv_x3": "conv_x3 (implicit-GEMM conv / GEMM, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
     "conv_x5": "conv_x5 (implicit-GEMM conv, LDS-DMA staging, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
-    "conv_x6": "conv_x6 (halo-reuse direct 3x3 conv, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
-    "gemm_lat": "gemm_lat (whole-K small GEMM, fp32 MFMA v_mfma_f32_16x16x4_f32)",
+    "conv_x6": "conv_x6 (halo-reuse direct 3x3 conv on v_mfma_f32_32x32x16_{f16 x3 | bf16})",
 }
-CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm", "gemm_lat")
+CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm")
+OTHER_KERNELS = ("stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample", "decoder", "misc")
 DTYPE = {
     "fp32": "fp32",
     "f16x3": "fp32 via f16x3 (each fp32 operand = hi+lo fp16, products ah*bh+ah*bl+al*bh, fp32 accumulate)",
+    "bf16": "bf16 (one bf16 product per MAC, fp32 accumulate; reduced precision)",
 }
 
 
@@ -53,34 +70,66 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=64, help="scenes per GPU")
     p.add_argument("--denoise-steps", type=int, default=2)
-    p.add_argument("--cpu-sample", type=int, default=64, help="scenes in the CPU-oracle baseline sample")
-    p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", default="8,16", help="thread counts of the CPU-oracle baseline")
     p.add_argument("--arch", default="resnet34")
-    p.add_argument("--gemm", default="f16x3", choices=["fp32", "f16x3"],
-                   help="conv/linear arithmetic: fp32 MFMA or the fp32-class 3-product fp16 split")
-    p.add_argument("--no-compare", action="store_true", help="skip the fp32-path comparison timing")
+    p.add_argument("--gemm", default="f16x3", choices=["fp32", "f16x3", "bf16"],
+                   help="conv/linear arithmetic: fp32 MFMA, the fp32-class 3-product fp16 split, or bf16")
+    p.add_argument("--no-compare", action="store_true", help="skip the fp32 leg and the H2D-inclusive leg")
+    p.add_argument("--cpu-plumbing", action="store_true",
+                   help="tests only: launcher + gloo all_gather + JSON with a stand-in step (no forward)")
     return p.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script (before any GPU call in this process) and return the
+    worst exit code. Rank 0's stdout carries the JSON line."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} disagrees with WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_plumbing:
+        return plumbing(args, world, rank)
+
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        world = dist.get_world_size()  # the world the RCCL communicator actually formed
     else:
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{local}")
 
     from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.dist import ScenePlanner
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
 
@@ -90,33 +139,43 @@ def main():
     model.set_gemm_mode(args.gemm)
     B = args.batch
     inp = synthetic_inputs(B, 1234 + rank, cfg)
-    feats = {k: torch.from_numpy(inp[k]).to(dev) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    keys = ("camera_feature", "lidar_feature", "status_feature")
+    feats = {k: torch.from_numpy(inp[k]).to(dev) for k in keys}
     noise = torch.from_numpy(inp["noise"]).to(dev)
-    from diffusiondrive_amd.dist import ScenePlanner
     planner = ScenePlanner(lambda f, nz: model.forward(f, noise=nz, steps=args.denoise_steps)["trajectory"])
 
     def step():
         # per-rank shard of the global batch (weak scaling) + one RCCL all_gather of trajectories
         return planner.gather(planner.fn(feats, noise))
 
+    def timed(fn, k):
+        """k steps between barrier + synchronize; per-step HIP events on the current stream."""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev[0].record()
+        o = None
+        for i in range(k):
+            o = fn()
+            ev[i + 1].record()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        per = [ev[i].elapsed_time(ev[i + 1]) for i in range(k)]
+        return o, el, per
+
     for _ in range(args.warmup):
         out = step()
     torch.cuda.synchronize()
-
+    out, elapsed, per_step = timed(step, args.steps)
+    med = float(np.median(per_step))
     if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, med], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, med = float(t[0].item()), float(t[1].item())
     ms_per_step = elapsed / args.steps * 1e3
     scenes_per_s = B * world * args.steps / elapsed
     traj_gpu = out[rank * B:(rank + 1) * B].detach().cpu().numpy()
@@ -125,8 +184,8 @@ def main():
         print(f"[bench] WARNING: numerics flags {num_flags:#x} raised (f16x3 overflow): result untrustworthy",
               file=sys.stderr)
 
-    # ---- roofline of the dominant kernel: a profiled replay of the same workload (HIP events
-    # around every conv_gemm launch on the handle's stream)
+    # ---- roofline of the dominant kernel: a profiled single-stream replay of the same workload
+    # (HIP events around every launch on the stream it is issued to)
     model.set_profiling(True)
     model.reset_stats()
     prof_steps = max(1, min(args.steps, 5))
@@ -136,33 +195,49 @@ def main():
     conv_stats = {k: model.kernel_stats(k) for k in CONV_KERNELS}
     main_k = max(CONV_KERNELS, key=lambda k: conv_stats[k]["ms"])
     st = conv_stats[main_k]
-    other = {k: model.kernel_stats(k) for k in ("stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
-                                                 "misc")}
+    other = {k: model.kernel_stats(k) for k in OTHER_KERNELS}
     other.update({k: v for k, v in conv_stats.items() if k != main_k})
     model.set_profiling(False)
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["flops"] / max(st["launches"], 1)
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     total_prof_ms = st["ms"] + sum(v["ms"] for v in other.values())
+    executed_flops = sum(v["flops"] for v in conv_stats.values()) + other["attn"]["flops"]
+    executed_gflop_scene = executed_flops / prof_steps / B / 1e9
 
-    # the other gemm mode on the same workload, for comparison (rank 0 view, N = 1 only)
-    compare = None
+    fp32_leg = h2d = None
     if world == 1 and not args.no_compare:
-        other_mode = "fp32" if args.gemm == "f16x3" else "f16x3"
+        # the fp32-MFMA path on the same workload (the conservative headline)
+        other_mode = "fp32" if args.gemm != "fp32" else "f16x3"
         model.set_gemm_mode(other_mode)
         for _ in range(2):
-            o2 = step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        n_cmp = max(3, args.steps // 2)
-        for _ in range(n_cmp):
-            o2 = step()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        d = (o2.detach().cpu().numpy()[..., :2].astype(np.float64) - traj_gpu[..., :2]).reshape(B, -1)
-        compare = {"gemm": other_mode, "value": round(B * n_cmp / dt, 3), "ms_per_step": round(dt / n_cmp * 1e3, 3),
-                   "steps": n_cmp, "waypoint_l2_vs_primary": float(np.sqrt((d ** 2).sum(-1)).max())}
+            step()
+        n_cmp = max(5, args.steps // 2)
+        o2, dt, per2 = timed(step, n_cmp)
+        fp32_leg = {"gemm": other_mode, "value": round(B * n_cmp / dt, 3), "ms_per_step": round(dt / n_cmp * 1e3, 3),
+                    "median_ms_per_step": round(float(np.median(per2)), 3), "steps": n_cmp,
+                    "traj": o2.detach().cpu().numpy()}
         model.set_gemm_mode(args.gemm)
+        # PCIe-inclusive: inputs staged from pinned host memory every step
+        host = {k: torch.from_numpy(inp[k]).pin_memory() for k in keys}
+        host_nz = torch.from_numpy(inp["noise"]).pin_memory()
+        dbuf = {k: torch.empty_like(v, device=dev) for k, v in host.items()}
+        dnz = torch.empty_like(host_nz, device=dev)
+
+        def step_h2d():
+            for k in keys:
+                dbuf[k].copy_(host[k], non_blocking=True)
+            dnz.copy_(host_nz, non_blocking=True)
+            return model.forward(dbuf, noise=dnz, steps=args.denoise_steps)["trajectory"]
+
+        for _ in range(2):
+            step_h2d()
+        n_h = max(5, args.steps // 2)
+        _, dt, per3 = timed(step_h2d, n_h)
+        h2d = {"value": round(B * n_h / dt, 3), "ms_per_step": round(dt / n_h * 1e3, 3),
+               "median_ms_per_step": round(float(np.median(per3)), 3), "steps": n_h,
+               "bytes_per_step": int(sum(v.numel() * 4 for v in host.values()) + host_nz.numel() * 4),
+               "note": "inputs copied host(pinned)->HBM inside every step; not the headline value"}
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{main_k}_{args.gemm}.json")
@@ -170,17 +245,18 @@ def main():
         try:
             with open(pmc_path) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
-        except Exception:
+        except (OSError, ValueError):
             traffic = None
 
     result = {
-        "metric": "scenes/s at batch 64, 2 denoise steps, 1/2/4/8 MI355X; waypoint L2 vs ref",
+        "metric": METRIC,
         "value": round(scenes_per_s, 3),
         "unit": "scenes/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
+        "median_ms_per_step": round(med, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -204,10 +280,11 @@ def main():
             "peak": round(ALGO_PEAK[args.gemm], 1),
             "unit": "TFLOP/s",
             "frac": round(achieved / ALGO_PEAK[args.gemm], 4),
-            "peak_note": "algorithmic fp32 FLOP/s ceiling: fp32 MFMA 157.3 TF" if args.gemm == "fp32" else
-                         "algorithmic fp32 FLOP/s ceiling: dense f16 MFMA 2500 TF / 3 products per fp32 MAC",
-            "achieved_vs_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "peak_note": {"fp32": "fp32 MFMA 157.3 TF",
+                          "f16x3": "algorithmic fp32 FLOP/s ceiling: dense f16 MFMA 2500 TF / 3 products per fp32 MAC",
+                          "bf16": "dense bf16 MFMA 2500 TF"}[args.gemm],
             "traffic": traffic,
+            "traffic_source": os.path.relpath(pmc_path, ROOT) if traffic is not None else None,
             "launches_per_step": st["launches"] // prof_steps,
             "avg_launch_ms": round(avg_ms, 5),
             "gflop_per_launch": round(flops_per_launch / 1e9, 4),
@@ -220,44 +297,70 @@ def main():
         },
         "device_ms_per_step": {k: round(v["ms"] / prof_steps, 4) for k, v in
                                sorted({main_k: st, **other}.items(), key=lambda kv: -kv[1]["ms"]) if v["launches"]},
+        "launches_per_step": {k: v["launches"] // prof_steps for k, v in {main_k: st, **other}.items()
+                              if v["launches"]},
         "whole_forward": {
-            "gflop_per_scene": CANONICAL_GFLOP_PER_SCENE_2STEP if args.denoise_steps == 2 else None,
-            "tflops": round(scenes_per_s / world * CANONICAL_GFLOP_PER_SCENE_2STEP / 1e3, 3)
+            "canonical_gflop_per_scene": CANONICAL_GFLOP_PER_SCENE_2STEP if args.denoise_steps == 2 else None,
+            "canonical_tflops": round(scenes_per_s / world * CANONICAL_GFLOP_PER_SCENE_2STEP / 1e3, 3)
             if args.denoise_steps == 2 else None,
+            "executed_gflop_per_scene": round(executed_gflop_scene, 3),
+            "executed_tflops": round(scenes_per_s / world * executed_gflop_scene / 1e3, 3),
+            "note": "canonical = SURVEY §8d algorithmic work; executed = the GEMM/conv/attention FLOPs the graph "
+                    "issues (value_proj only at the sampled taps, bev_proj keyval half at 8x8)",
         },
+        "numerics_flags": num_flags,
     }
-    if result["whole_forward"]["tflops"] is not None:
-        result["whole_forward"]["frac_of_fp32_peak"] = round(result["whole_forward"]["tflops"] / FP32_MFMA_PEAK_TFLOPS,
-                                                             4)
-
-    result["numerics_flags"] = num_flags
-    if compare is not None:
-        result["compare_gemm_mode"] = compare
+    if h2d is not None:
+        result["h2d_included"] = h2d
+    cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, cfg, sd, inp, traj_gpu)
+        cpu, ref = cpu_baseline(args, cfg, sd, inp)
+        cpu["waypoint_l2_gpu_vs_oracle"] = waypoint_l2(traj_gpu, ref)
+        if fp32_leg is not None:
+            fp32_leg["waypoint_l2_vs_oracle"] = waypoint_l2(fp32_leg["traj"], ref)
+        result["waypoint_l2_vs_oracle"] = cpu["waypoint_l2_gpu_vs_oracle"]
+    if fp32_leg is not None:
+        fp32_leg["waypoint_l2_vs_primary"] = waypoint_l2(fp32_leg.pop("traj"), traj_gpu)
+        result["fp32_leg"] = fp32_leg
+    if cpu is not None:
+        result["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, cfg, sd, inp, traj_gpu):
-    """Golden-pinned CPU oracle on a bounded sample (first `cpu_sample` scenes of the batch)."""
+def waypoint_l2(a, b):
+    d = (np.asarray(a, np.float64)[..., :2] - np.asarray(b, np.float64)[..., :2]).reshape(len(a), -1)
+    return float(np.sqrt((d ** 2).sum(-1)).max())
+
+
+def cpu_baseline(args, cfg, sd, inp):
+    """Golden-pinned CPU oracle timed on this host: B = 64 (the metric's batch, one rep) and B = 1
+    (three reps) at each thread count of --cpu-threads. Returns (record, oracle trajectories of the
+    B = 64 sample)."""
     from oracle.model import OracleModel
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    S = min(args.cpu_sample, inp["status_feature"].shape[0])
     om = OracleModel(sd, cfg)
-    sl = {k: inp[k][:S] for k in ("camera_feature", "lidar_feature", "status_feature", "noise")}
-    om.forward(sl["camera_feature"][:1], sl["lidar_feature"][:1], sl["status_feature"][:1], sl["noise"][:1],
-               steps=args.denoise_steps, heads=False)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_reps):
-        ref = om.forward(sl["camera_feature"], sl["lidar_feature"], sl["status_feature"], sl["noise"],
-                         steps=args.denoise_steps, heads=False)["trajectory"].numpy()
-    dt = time.perf_counter() - t0
-    d = (traj_gpu[:S, :, :2].astype(np.float64) - ref[..., :2].astype(np.float64)).reshape(S, -1)
-    l2 = float(np.sqrt((d ** 2).sum(-1)).max())
+    S = inp["status_feature"].shape[0]
+    keys = ("camera_feature", "lidar_feature", "status_feature", "noise")
+
+    def run(n):
+        return om.forward(*(inp[k][:n] for k in keys), steps=args.denoise_steps, heads=False)["trajectory"].numpy()
+
+    threads = [int(t) for t in args.cpu_threads.split(",") if t]
+    grid, ref = {}, None
+    for n_t in threads:
+        torch.set_num_threads(n_t)
+        run(1)  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(3):
+            run(1)
+        b1 = 3 / (time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        ref = run(S)
+        bs = S / (time.perf_counter() - t0)
+        grid[f"threads={n_t}"] = {f"B={S}": round(bs, 4), "B=1": round(b1, 4)}
+    head = max(threads)
     cpu_name = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -267,16 +370,54 @@ def cpu_baseline(args, cfg, sd, inp, traj_gpu):
                     break
     except OSError:
         pass
-    return {
-        "value": round(S * args.cpu_reps / dt, 4),
+    rec = {
+        "value": grid[f"threads={head}"][f"B={S}"],
         "unit": "scenes/s",
-        "cores": threads,
+        "cores": head,
         "kind": "port",
-        "sample": f"{S} scenes x {args.cpu_reps} reps of the same synthetic batch (oracle/model.py, PyTorch-CPU "
-                  f"fp32, {threads} threads, {cpu_name})",
-        "seconds": round(dt, 2),
-        "waypoint_l2_gpu_vs_oracle": l2,
+        "sample": f"{S} scenes x 1 rep (and 1 scene x 3 reps) of the same synthetic batch per thread count "
+                  f"(oracle/model.py, PyTorch-CPU fp32, {cpu_name}; {os.cpu_count()} host CPUs visible, "
+                  f"{head} = this job's CPU share)",
+        "grid": grid,
     }
+    return rec, ref
+
+
+def plumbing(args, world, rank):
+    """CPU stand-in for the multi-rank path (tests): gloo process group, the same ScenePlanner
+    all_gather, barrier + max-over-ranks timing, rank-0 JSON. The step is a stand-in (zeros)."""
+    import torch.distributed as dist
+    from diffusiondrive_amd.dist import ScenePlanner
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    B = args.batch
+    planner = ScenePlanner(lambda f, nz: torch.full((B, 8, 3), float(rank)))
+    for _ in range(args.warmup):
+        planner.gather(planner.fn(None, None))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = planner.gather(planner.fn(None, None))
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ranks_seen = sorted({int(v) for v in out[:, 0, 0].tolist()})
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(B * world * args.steps / el, 3), "unit": "scenes/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "none",
+                          "data": "plumbing test: stand-in step, no forward (CPU, gloo)",
+                          "config": {"workload": "plumbing", "batch_per_gpu": B, "global_batch": B * world,
+                                     "gathered_rows": int(out.shape[0]), "ranks_seen": ranks_seen}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

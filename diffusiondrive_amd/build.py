@@ -17,7 +17,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libddmi.so")
 ARCH = os.environ.get("DDMI_ARCH", "gfx950")
-SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "attention.hip", "gemm_lat.hip", "stem_pool.hip", "features.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
+SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "attention.hip", "stem_pool.hip", "features.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", CSRC, "-I", INCLUDE]
 # Elementwise / decoder arithmetic must round like PyTorch-CPU's separate mul and add kernels

@@ -43,8 +43,7 @@ __device__ inline float at_wave_sum(float v) {
 
 constexpr int kQB = 64;  // query rows per workgroup (4 tiles of 16)
 
-// DBG (timing experiments only, results wrong): 1 skip phase 1, 2 skip phase 2, 4 skip phase 3
-template <int HS, int DBG = 0>
+template <int HS>
 __global__ __launch_bounds__(256) void gpt_attn_kernel(const float* __restrict__ qkv, float* __restrict__ y, int T,
                                                        int C, int heads, int nqb, float scale) {
   constexpr int KQ = HS / 4;                // k slice per lane group in phase 1
@@ -70,7 +69,7 @@ __global__ __launch_bounds__(256) void gpt_attn_kernel(const float* __restrict__
   const int q0 = qb * kQB;
 
   // ---- phase 1: scores
-  if constexpr (!(DBG & 1)) {
+  {
     const float* qp = base + (int64_t)(q0 + r) * ld + g * KQ;  // + 16 mt ld
     at_f4 qf[4][KC / 4];
     auto load_q = [&](int ch) {
@@ -127,7 +126,7 @@ __global__ __launch_bounds__(256) void gpt_attn_kernel(const float* __restrict__
   // ---- phase 2: row softmax of scale * s. Four threads per row, each holding a quarter of it in
   // registers (16-B LDS reads / writes), the row max / sum combined over the 4 lanes by 2 xor steps:
   // no dependent wave-wide reduction chains (what a row-per-wave softmax is bound by here).
-  if constexpr (!(DBG & 2)) {
+  {
     constexpr int QMAX = 512 / 16;  // float4 per thread at T <= 512
     const int row = threadIdx.x >> 2, seg = threadIdx.x & 3;
     const int nq = T / 16;          // float4 per thread
@@ -168,7 +167,6 @@ __global__ __launch_bounds__(256) void gpt_attn_kernel(const float* __restrict__
   constexpr int MG = NN >= 4 ? 4 : NN;  // query tiles per unit
   constexpr int NU = NN * (4 / MG);     // units
   const int KT = T / 4;                 // keys per lane group
-  if constexpr (!(DBG & 4))
   for (int u = wave; u < NU; u += 4) {
     const int ct = u % NN, m0 = (u / NN) * MG;
     const float* pr = S + (m0 * 16 + r) * ldS;  // row & 15 == r for every query tile
@@ -223,18 +221,10 @@ void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, floa
   const size_t lds = (size_t)kQB * T * sizeof(float);
   const float scale = (float)(1.0 / std::sqrt((double)hs));  // math.sqrt in the reference
   const dim3 grid((unsigned)((int64_t)B * heads * nqb)), block(256);
-  static const int dbg = getenv("DDMI_ATT_DBG") ? atoi(getenv("DDMI_ATT_DBG")) : 0;
   switch (hs) {
-#define AT(HS)                                                                                                \
-  case HS:                                                                                                    \
-    if (dbg == 0)                                                                                             \
-      hipLaunchKernelGGL((gpt_attn_kernel<HS, 0>), grid, block, lds, st, qkv, y, T, C, heads, nqb, scale);    \
-    else if (dbg == 1)                                                                                        \
-      hipLaunchKernelGGL((gpt_attn_kernel<HS, 1>), grid, block, lds, st, qkv, y, T, C, heads, nqb, scale);    \
-    else if (dbg == 4)                                                                                        \
-      hipLaunchKernelGGL((gpt_attn_kernel<HS, 4>), grid, block, lds, st, qkv, y, T, C, heads, nqb, scale);    \
-    else                                                                                                      \
-      hipLaunchKernelGGL((gpt_attn_kernel<HS, 6>), grid, block, lds, st, qkv, y, T, C, heads, nqb, scale);    \
+#define AT(HS)                                                                                          \
+  case HS:                                                                                              \
+    hipLaunchKernelGGL((gpt_attn_kernel<HS>), grid, block, lds, st, qkv, y, T, C, heads, nqb, scale); \
     break;
     AT(16) AT(32) AT(64) AT(128) AT(256) AT(512)
 #undef AT

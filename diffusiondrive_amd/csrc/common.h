@@ -77,6 +77,10 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
 // name of the kernel the last conv / GEMM dispatch on this thread went to ("conv_gemm", "conv_x3",
 // "conv_x5", "conv_x6"); the runtime's profiler attributes launch time per kernel with it
 const char* last_conv_kernel();
+// the kernel + tile configuration of the calling thread's last conv / GEMM launch, e.g.
+// "conv_x6<8,32,128,4,2>" (TH, TW, BN, wave grid), "conv_x5<256,256>", "conv_x3<128,128,f16x3>"
+const char* last_conv_config();
+void set_last_conv_config(const char* cfg);
 
 // ----------------------------------------------------------------------------------------
 // Bandwidth / small kernels (elementwise.hip)
@@ -93,12 +97,6 @@ void launch_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow,
 // out[n,y,x,c] (= or +=) bilinear(in)[n,y,x,c]. ratio_h/ratio_w = in/out unless a scale factor is given.
 void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float ratio_h,
                      float ratio_w, int accumulate, hipStream_t st);
-// cross_bev = LN(ReLU(W p3 + bias + bilinear(kvp))) in one pass (elementwise.hip): p3 (B, H, 64, 64) strided,
-// kvp (B, Hk, Wk, 256) contiguous, w = the p3 columns of the projection (row stride ldw), out (B, H, 64, 256).
-// False (nothing launched) outside C = 256, 64 p3 channels, W = 64, Wk <= 8.
-bool launch_bevproj_fused(const float* p3, int64_t p3_sn, int64_t p3_sh, int64_t p3_sw, int Kp3, const float* kvp,
-                          int Hk, int Wk, const float* w, int ldw, const float* bias, const float* g, const float* be,
-                          float* out, int B, int H, int W, int C, hipStream_t st);
 // Row LayerNorm (eps 1e-5): y[r] = LN(x[r] + res[r / res_div]) * g + b, then optional FiLM
 // y = y * (1 + film_scale) + film_shift. C <= 2048. In-place allowed (y == x).
 void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldres, int res_div,
@@ -158,11 +156,6 @@ void launch_mha_small(const float* q, int64_t ldq, const float* k, const float* 
                       int64_t q_bstride, int64_t kv_bstride, int64_t o_bstride, hipStream_t st);
 // reg (rows, P, 3) from the raw branch output r (rows, P*3): xy += pts, heading = tanh * pi;
 // optionally also writes the cascade's next points (rows, P, 2).
-// Fused reg branch (Linear nin->nhid, ReLU, Linear nhid->nhid, ReLU, Linear nhid->nout) + the finalize below, fp32
-// VALU; false (nothing launched) unless nin = nhid = 256 and nout = P * 3 <= 32 (decoder.hip).
-bool launch_reg_mlp(const float* x, int64_t ldx, const float* w0, const float* b0, const float* w2, const float* b2,
-                    const float* w4, const float* b4, int nin, int nhid, int nout, const float* pts, float* reg,
-                    float* pts_next, int rows, int P, hipStream_t st);
 void launch_reg_finalize(const float* r, const float* pts, float* reg, float* pts_next, int rows, int P,
                          hipStream_t st);
 // img = DDIM.step(norm_odo(reg[..., :2]), t -> t-1, img), eta = 0, prediction 'sample', clip.

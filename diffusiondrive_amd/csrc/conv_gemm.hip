@@ -265,21 +265,14 @@ static void launch_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 
 void set_last_conv_kernel(const char* k);  // conv_x3.hip
 
-void set_last_conv_kernel(const char* k);                  // conv_x3.hip
-bool launch_gemm_lat(const ConvArgs& a, hipStream_t st);  // gemm_lat.hip
-
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st) {
-  // small latency-bound GEMMs / 1x1 convs: exact-fp32 whole-K kernel (fp32 and f16x3 modes)
   if (a.rowmap && !a.wh) throw std::runtime_error("conv_gemm: gathered rows need the f16x3 kernel (conv_x3)");
-  if (!a.rowmap && (!a.wh || a.prec == 0) && launch_gemm_lat(a, st)) {
-    set_last_conv_kernel("gemm_lat");
-    return;
-  }
   if (a.wh) {
     launch_conv_x3(a, st);
     return;
   }
   set_last_conv_kernel("conv_gemm");
+  set_last_conv_config("conv_gemm");
   if (a.Cin % 4 != 0) throw std::runtime_error("conv_gemm: Cin must be a multiple of 4");
   if ((a.in_sw % 4) || (a.in_sh % 4) || (a.in_sn % 4) || (reinterpret_cast<uintptr_t>(a.in) % 16))
     throw std::runtime_error("conv_gemm: input strides / base must be 16-byte aligned");

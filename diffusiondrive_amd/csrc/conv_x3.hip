@@ -28,7 +28,6 @@
 //  * Double-buffered LDS; chunk k+1's global loads are in flight during chunk k's MFMAs.
 //  * XCD-aware bijective tile remap (blocks b, b+8, ... share an XCD's L2 -> consecutive tiles).
 //  * Fused epilogue: per-channel weight scale, alpha, bias, residual, ReLU, strided NHWC store.
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -58,7 +57,7 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0, int DBG = 0, int SCHED = 0>
+template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 - a 32-wide K chunk lies inside one filter tap, the
@@ -230,17 +229,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const float4 v = ra[S][i];
-      if constexpr (DBG & 8) continue;
       if constexpr (PREC == 1) {
         const bf16x2 b01 = __builtin_convertvector((float2_t){v.x, v.y}, bf16x2);
         const bf16x2 b23 = __builtin_convertvector((float2_t){v.z, v.w}, bf16x2);
         *reinterpret_cast<uint2*>(sah + a_woff[i]) =
             make_uint2(__builtin_bit_cast(uint32_t, b01), __builtin_bit_cast(uint32_t, b23));
-        continue;
-      }
-      if constexpr (DBG & 1) {  // experiment: raw bits, no split arithmetic
-        *reinterpret_cast<uint2*>(sah + a_woff[i]) = make_uint2(__builtin_bit_cast(uint32_t, v.x), __builtin_bit_cast(uint32_t, v.y));
-        *reinterpret_cast<uint2*>(sal + a_woff[i]) = make_uint2(__builtin_bit_cast(uint32_t, v.z), __builtin_bit_cast(uint32_t, v.w));
         continue;
       }
       const half2_t h01 = __builtin_convertvector((float2_t){v.x, v.y}, half2_t);
@@ -256,10 +249,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      if constexpr (DBG & 2) {
-        asm volatile("" ::"v"(rbh[S][j].x), "v"(rbl[S][j].x));
-        continue;
-      }
       *reinterpret_cast<uint4*>(sbh + b_woff[j]) = rbh[S][j];
       if constexpr (PREC == 0) *reinterpret_cast<uint4*>(sbl + b_woff[j]) = rbl[S][j];
     }
@@ -325,11 +314,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      if constexpr (DBG & 16) {  // experiment: no fragment reads
-        for (int j = 0; j < TN; ++j) bh[s2][j] = bl[s2][j] = (half8){};
-        for (int i = 0; i < TM; ++i) ah[s2][i] = al[s2][i] = (half8){};
-        continue;
-      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bh[s2][j] = *reinterpret_cast<const half8*>(sbh + b_roff[s2][j]);
@@ -340,13 +324,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
         ah[s2][i] = *reinterpret_cast<const half8*>(sah + a_roff[s2][i]);
         al[s2][i] = *reinterpret_cast<const half8*>(sal + a_roff[s2][i]);
       }
-    }
-    if constexpr (DBG & 4) {  // experiment: no MFMAs (fragments kept live)
-      for (int s2 = 0; s2 < 2; ++s2) {
-        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(ah[s2][i]), "v"(al[s2][i]));
-        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bh[s2][j]), "v"(bl[s2][j]));
-      }
-      return;
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -374,55 +351,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   // K loop runs to an even count): a conditional load would make hipcc's vmcnt bookkeeping fall
   // back to vmcnt(0) and drain the chunk kept in flight.
   auto iteration = [&](int kc, auto NEXT) {
-    if constexpr (SCHED == 0 || PREC == 1 || DBG != 0) {
-      compute(kc & 1);
-      store_chunk((kc + 1) & 1, NEXT);
-      load_chunk(NEXT, (kc + 3) * BK);
-    } else {
-      // fragment reads of this chunk first, then the staging of the next chunks, then the MFMAs:
-      // the LDS reads precede the LDS writes in program order (the compiler cannot prove the two
-      // buffers disjoint), and the MFMAs (register-only) are free to interleave with the staging.
-      const char* st = lds + (kc & 1) * STAGE;
-      const char* sah = st;
-      const char* sal = st + BM * ROWB;
-      const char* sbh = st + NIMG * BM * ROWB;
-      const char* sbl = st + (NIMG * BM + BN) * ROWB;
-      half8 ah[2][TM], al[2][TM], bh[2][TN], bl[2][TN];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          bh[s2][j] = *reinterpret_cast<const half8*>(sbh + b_roff[s2][j]);
-          bl[s2][j] = *reinterpret_cast<const half8*>(sbl + b_roff[s2][j]);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          ah[s2][i] = *reinterpret_cast<const half8*>(sah + a_roff[s2][i]);
-          al[s2][i] = *reinterpret_cast<const half8*>(sal + a_roff[s2][i]);
-        }
-      }
-      store_chunk((kc + 1) & 1, NEXT);
-      load_chunk(NEXT, (kc + 3) * BK);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2][i], bh[s2][j], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2][i], bl[s2][j], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2][i], bh[s2][j], acc[i][j], 0, 0, 0);
-      }
-      if constexpr (SCHED == 2) __builtin_amdgcn_iglp_opt(0);
-    }
+    compute(kc & 1);
+    store_chunk((kc + 1) & 1, NEXT);
+    load_chunk(NEXT, (kc + 3) * BK);
     __syncthreads();
   };
 
@@ -505,38 +436,11 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   const int ntm = (M + BM - 1) / BM;
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
-  static const int dbg = getenv("DDMI_X3_DBG") ? atoi(getenv("DDMI_X3_DBG")) : 0;
-  static const int sched = getenv("DDMI_X3_SCHED") ? atoi(getenv("DDMI_X3_SCHED")) : 0;
-  if constexpr ((WM == 2 && WN == 2 && TM == 2 && TN == 2) || (WM == 4 && WN == 1 && TM == 2 && TN == 2)) {
-    if (sched && a.prec == 0 && a.Cin % BK == 0 && a.KH * a.KW <= 32) {
-#define DD_SCH(V)                                                                                          \
-  case V:                                                                                                  \
-    hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1, 0, 0, V>), grid, dim3(64 * WM * WN), 0, st, a, M, K, \
-                       ntm, ntn);                                                                          \
-    break;
-      switch (sched) {
-        DD_SCH(1) DD_SCH(2)
-        default: throw std::runtime_error("bad DDMI_X3_SCHED");
-      }
-#undef DD_SCH
-      DD_HIP_CHECK(hipGetLastError());
-      return;
-    }
-  }
-  if constexpr (WM == 2 && WN == 2 && TM == 2 && TN == 2) {
-    if (dbg && a.prec == 0 && a.Cin % BK == 0 && a.KH * a.KW <= 32) {
-#define DD_DBG(D) \
-  case D: hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, 1, 0, D>), grid, dim3(256), 0, st, a, M, K, ntm, ntn); break;
-      switch (dbg) {
-        DD_DBG(1) DD_DBG(2) DD_DBG(3) DD_DBG(4) DD_DBG(8) DD_DBG(10) DD_DBG(16) DD_DBG(11) DD_DBG(20)
-        default: throw std::runtime_error("bad DDMI_X3_DBG");
-      }
-#undef DD_DBG
-      DD_HIP_CHECK(hipGetLastError());
-      return;
-    }
-  }
   const bool walk = a.Cin % BK == 0 && a.KH * a.KW <= 32;
+  static const std::string name[2] = {
+      "conv_x3<" + std::to_string(BM) + "," + std::to_string(BN) + ",f16x3>",
+      "conv_x3<" + std::to_string(BM) + "," + std::to_string(BN) + ",bf16>"};
+  set_last_conv_config(name[a.prec == 1].c_str());
   if (a.prec == 1) {
     if (walk)
       hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
@@ -556,6 +460,9 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st);                 // conv_
 static thread_local const char* g_last_conv = "conv_gemm";
 const char* last_conv_kernel() { return g_last_conv; }
 void set_last_conv_kernel(const char* k) { g_last_conv = k; }
+static thread_local const char* g_last_cfg = "";
+const char* last_conv_config() { return g_last_cfg; }
+void set_last_conv_config(const char* c) { g_last_cfg = c; }
 
 void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if (a.Cin % 4 != 0) throw std::runtime_error("conv_x3: Cin must be a multiple of 4");
@@ -582,43 +489,27 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
     throw std::runtime_error("conv_x3: per-image output extent too large");
   // default f16x3 path: 3x3 stride-1 convs on the halo-reuse direct kernel (conv_x6.hip), other
   // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
-  static const int use_x6 = getenv("DDMI_X6") ? atoi(getenv("DDMI_X6")) : 1;
   if (a.rowmap) {
     g_last_conv = "conv_x3";
-    static const int gt = getenv("DDMI_GATHER_TILE") ? atoi(getenv("DDMI_GATHER_TILE")) : 0;
-    if (gt == 1)
-      launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
-    else if (gt == 2)
-      launch_x3_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64
-    else if (gt == 3)
-      launch_x3_cfg<2, 2, 1, 2>(a, M, K, st);  // 64 x 128
-    else
-      launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);  // 128 x 128
+    launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);  // gathered rows: 128 x 128
     return;
   }
-  if (use_x6 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x6(a, st)) {
+  if (launch_conv_x6(a, st)) {
     g_last_conv = "conv_x6";
     return;
   }
-  static const int use_x5 = getenv("DDMI_X5") ? atoi(getenv("DDMI_X5")) : 1;
-  if (use_x5 && a.prec == 0 && !getenv("DDMI_X3_DBG") && !getenv("DDMI_X3_SCHED") && launch_conv_x5(a, M, K, st)) {
+  if (a.prec == 0 && launch_conv_x5(a, M, K, st)) {
     g_last_conv = "conv_x5";
     return;
   }
   g_last_conv = "conv_x3";
   const int64_t t128 = ((M + 127) / 128) * (int64_t)((a.Cout + 127) / 128);
-  const int64_t t256 = ((M + 255) / 256) * (int64_t)((a.Cout + 127) / 128);
-  static const int big = getenv("DDMI_X3_BIG") ? atoi(getenv("DDMI_X3_BIG")) : 0;
   const bool generic = !(a.Cin % BK == 0 && a.KH * a.KW <= 32);
   if (a.Cout <= 64) {
     if (!generic && (M + 255) / 256 >= 256)
       launch_x3_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64
     else
       launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
-  } else if (big == 1 && t256 >= 256) {
-    launch_x3_cfg<2, 2, 4, 2>(a, M, K, st);    // 256 x 128, one 4-wave WG per CU
-  } else if (big == 2 && t256 >= 256) {
-    launch_x3_cfg<4, 2, 2, 2>(a, M, K, st);    // 256 x 128, one 8-wave WG per CU
   } else if (t128 >= 512) {
     launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);    // 128 x 128
   } else {

@@ -353,6 +353,8 @@ static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   const int ntm = (M + BM - 1) / BM;
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
+  static const std::string name = "conv_x5<" + std::to_string(BM) + "," + std::to_string(BN) + ">";
+  set_last_conv_config(name.c_str());
   if (a.Cin % KC == 0 && a.KH * a.KW <= 32)
     hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
   else
@@ -361,23 +363,19 @@ static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 }
 
 // Returns false when the shape is better served by conv_x3 (grids too small to fill the chip).
-// Tiles: 256 x 256 with 2 stages (128 KB), 256 x 128 / 256 x 64 with 3 (144 / 96 KB).
-// DDMI_X5_WIDE=1 also routes the Cout > 128 grids that only fill the chip at 256 x 128, and the
-// mid-size GEMMs at 128 x 128 (4 waves, 3 stages): measured slower than conv_x3's 128 x 128 /
-// 64 x 64 on the GPT shapes (tools/micro/gemm_x3_bench.py), so off by default.
+// Tiles: 256 x 256 with 2 stages (128 KB), 256 x 128 / 256 x 64 with 3 (144 / 96 KB). The Cout > 128
+// grids that fill the chip only at 256 x 128, and 128 x 128 tiles for the mid-size GEMMs, measured
+// slower than conv_x3 on the GPT shapes (tools/micro/gemm_x3_bench.py) and are not routed here.
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
-  static const int mode = getenv("DDMI_X5_WIDE") ? atoi(getenv("DDMI_X5_WIDE")) : 0;
-  const int64_t m256 = (M + 255) / 256, m128 = (M + 127) / 128;
+  const int64_t m256 = (M + 255) / 256;
   const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;
   if (a.Cout <= 64) {
     if (m256 < 256) return false;
     launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st);  // 256 x 64, 4 waves
   } else if (a.Cout > 128 && m256 * n256 >= 256) {
     launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);  // 256 x 256, 8 waves
-  } else if ((a.Cout <= 128 || mode) && m256 * n128 >= 256) {
+  } else if (a.Cout <= 128 && m256 * n128 >= 256) {
     launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);  // 256 x 128, 8 waves
-  } else if (mode && m128 * n128 >= 256 && K >= 128) {
-    launch_x5_cfg<2, 2, 2, 2, 3>(a, M, K, st);  // 128 x 128, 4 waves
   } else {
     return false;
   }

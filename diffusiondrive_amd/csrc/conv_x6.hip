@@ -113,9 +113,7 @@ constexpr bool halo_in_window(int t, int D, int TA, bool first) {
 // barrier that retires every wave's last read of the current one), so a 4-wave BN = 64 workgroup
 // fits twice per CU (66 KB of LDS) and one workgroup's prologue / epilogue runs beside the other's
 // MFMAs.
-// DBG (timing experiments only, results wrong): 1 no MFMA, 2 no B DMA, 4 no halo, 8 no fragment
-// reads, 16 no per-step barrier.
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int DBG = 0>
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
 __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks) {
   constexpr int NW = WM * WN, NT = 64 * NW;
@@ -192,7 +190,6 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   }
   x6f4 hr[ALD];
   auto halo_issue = [&](int c) {
-    if constexpr (DBG & 4) return;
     const bool cv = c < nchunks;
     const int co = c * 32;
 #pragma unroll
@@ -206,7 +203,6 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     for (int i = 0; i < ALD; ++i) asm volatile("" : "+v"(hr[i]));
   };
   auto halo_store = [&](int buf) {
-    if constexpr (DBG & 4) return;
     char* base = lds + buf * ABYTES;
 #pragma unroll
     for (int i = 0; i < ALD; ++i) {
@@ -237,7 +233,6 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   const bool bimg_lo = (wave * BPS) / BQ == 1;
   const x6i4 rwb = rsrc6(bimg_lo ? (const void*)a.wl : (const void*)a.wh);
   auto b_issue = [&](int slot, int tap, int c) {
-    if constexpr (DBG & 2) return;
     const bool cv = c < nchunks;
     const uint32_t kb = (uint32_t)(tap * Cin + c * 32) * 2u;
 #pragma unroll
@@ -281,11 +276,6 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   auto load_frag = [&](Frag& F, int slot, int c, auto TAP, auto S2) {
     constexpr int t = decltype(TAP)::value, s2 = decltype(S2)::value;
     constexpr int kh = t / 3, kw = t % 3;
-    if constexpr (DBG & 8) {
-      for (int j = 0; j < TN; ++j) F.bh[j] = F.bl[j] = (x6h8){};
-      for (int i = 0; i < TM; ++i) F.ah[i] = F.al[i] = (x6h8){};
-      return;
-    }
     const char* abuf = lds + (SH ? 0 : (c & 1)) * ABYTES + kh * P * 128;
     const char* bbuf = lds + B_OFF + slot * BSLOT;
 #pragma unroll
@@ -302,11 +292,6 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     }
   };
   auto mfma_frag = [&](const Frag& F) {
-    if constexpr (DBG & 1) {
-      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(F.ah[i]), "v"(F.al[i]));
-      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(F.bh[j]), "v"(F.bl[j]));
-      return;
-    }
     // small terms first, the hi x hi term last (independent accumulators interleaved)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -334,10 +319,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
     constexpr int N = (D - 1) * BPS + (halo_in_window(t, D, TA, first) ? ALD : 0);
-    if constexpr (DBG & 16)
-      wait_vm<N>();
-    else
-      step_barrier<N>();
+    step_barrier<N>();
     constexpr int tn = (t + D) % 9;
     int ns = slot + D;
     if (ns >= NSLOT) ns -= NSLOT;
@@ -468,24 +450,17 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int DBG = 0>
-static void launch_x6_one(const ConvArgs& a, hipStream_t st) {
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
+static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   const int n_sp = a.Nimg * tiles_x * tiles_y;
   const int ntn = (a.Cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, DBG>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0, st,
+  static const std::string name = "conv_x6<" + std::to_string(TH) + "," + std::to_string(TW) + "," +
+                                  std::to_string(BN) + "," + std::to_string(WM) + "," + std::to_string(WN) + ">";
+  set_last_conv_config(name.c_str());
+  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0, st,
                      a, tiles_x, tiles_y, n_sp, ntn, a.Cin / 32);
   DD_HIP_CHECK(hipGetLastError());
-}
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
-static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
-  static const int dbg = getenv("DDMI_X6_DBG") ? atoi(getenv("DDMI_X6_DBG")) : 0;
-  switch (dbg) {
-#define X6D(V) case V: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, V>(a, st); break;
-    X6D(0) X6D(1) X6D(2) X6D(4) X6D(8) X6D(16)
-#undef X6D
-    default: throw std::runtime_error("bad DDMI_X6_DBG");
-  }
 }
 
 // Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 conv this kernel covers (the
@@ -508,11 +483,10 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   const int64_t n_sp = (int64_t)a.Nimg * (wide ? ((a.Ho + 7) / 8) * ((a.Wo + 31) / 32)
                                                : ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16));
   const bool bn128 = a.Cout > 64 && n_sp * ((a.Cout + 127) / 128) >= 256;
-  static const int cfg = getenv("DDMI_X6_CFG") ? atoi(getenv("DDMI_X6_CFG")) : 0;
   // BN = 64 with Cin <= 64 (2 K chunks per tile: prologue / epilogue-heavy): 4-wave workgroups
   // (wave tile 64 x 64) with one halo buffer, two per CU - 12 % faster on the 64-channel layers,
-  // 11 % slower at Cin = 256 (tools/micro/conv_bench); cfg 2 forces the 8-wave form, cfg 3 the 4-wave
-  const bool sh4 = cfg == 3 || (cfg != 2 && a.Cin <= 64);
+  // 11 % slower at Cin = 256 (tools/micro/conv_bench)
+  const bool sh4 = a.Cin <= 64;
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   if (wide) {
     if (bn128) {

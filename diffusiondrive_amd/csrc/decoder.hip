@@ -517,101 +517,6 @@ void launch_reg_finalize(const float* r, const float* pts, float* reg, float* pt
   DD_HIP_CHECK(hipGetLastError());
 }
 
-// ---------------------------------------------------------------- fused reg branch + finalize
-// DiffMotionPlanningRefinementModule's reg branch (transfuser_model_v2.py:208-256: Linear 256->256, ReLU,
-// Linear 256->256, ReLU, Linear 256->P*3) and the decoder layer's epilogue (:375-382: reg[..., :2] +=
-// points, reg[..., 2] = tanh * pi) in one launch: a workgroup owns kRB mode rows, keeps them in LDS and
-// runs the per-query MLP on the VALU (thread j = output channel j; fp32 weights k-blocked [nin/4][nout][4]
-// so each wave load is one contiguous 1 KB segment from L2, activations as LDS broadcasts) - three 13 us
-// latency-bound GEMM launches + finalize -> one.
-constexpr int kRB = 8;
-
-__device__ inline void reg_dense256(const float (*in)[256], float (*out)[256], const float* __restrict__ w,
-                                    const float* __restrict__ b, int j) {
-  float acc[kRB];
-  const float bj = b ? b[j] : 0.f;
-#pragma unroll
-  for (int r = 0; r < kRB; ++r) acc[r] = 0.f;
-  // k-blocked weights [64][256][4]: lane j reads 16 B of a contiguous 1 KB row per k4 (coalesced)
-  const float4* wr = reinterpret_cast<const float4*>(w) + j;
-  for (int k4 = 0; k4 < 64; ++k4) {
-    const float4 wv = wr[k4 * 256];
-#pragma unroll
-    for (int r = 0; r < kRB; ++r) {
-      const float4 xv = *reinterpret_cast<const float4*>(&in[r][k4 * 4]);
-      acc[r] = __builtin_fmaf(wv.x, xv.x, acc[r]);
-      acc[r] = __builtin_fmaf(wv.y, xv.y, acc[r]);
-      acc[r] = __builtin_fmaf(wv.z, xv.z, acc[r]);
-      acc[r] = __builtin_fmaf(wv.w, xv.w, acc[r]);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < kRB; ++r) out[r][j] = fmaxf(acc[r] + bj, 0.f);
-}
-
-__global__ __launch_bounds__(256) void reg_mlp_kernel(const float* __restrict__ x, int64_t ldx,
-                                                      const float* __restrict__ w0, const float* __restrict__ b0,
-                                                      const float* __restrict__ w2, const float* __restrict__ b2,
-                                                      const float* __restrict__ w4, const float* __restrict__ b4,
-                                                      const float* __restrict__ pts, float* __restrict__ reg,
-                                                      float* __restrict__ pts_next, int rows, int P) {
-  __shared__ __attribute__((aligned(16))) float xa[kRB][256];
-  __shared__ __attribute__((aligned(16))) float xb[kRB][256];
-  const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * kRB;
-  for (int i = tid; i < kRB * 64; i += 256) {
-    const int r = i >> 6, c4 = (i & 63) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row0 + r < rows) v = *reinterpret_cast<const float4*>(x + (int64_t)(row0 + r) * ldx + c4);
-    *reinterpret_cast<float4*>(&xa[r][c4]) = v;
-  }
-  __syncthreads();
-  reg_dense256(xa, xb, w0, b0, tid);
-  __syncthreads();
-  reg_dense256(xb, xa, w2, b2, tid);
-  __syncthreads();
-  const int n4 = P * 3;
-  if (tid < kRB * n4) {
-    const int r = tid / n4, j = tid - r * n4;
-    const int row = row0 + r;
-    if (row < rows) {
-      float acc = 0.f;
-      const float4* wr = reinterpret_cast<const float4*>(w4) + j;
-      for (int k4 = 0; k4 < 64; ++k4) {
-        const float4 wv = wr[k4 * n4];
-        const float4 xv = *reinterpret_cast<const float4*>(&xa[r][k4 * 4]);
-        acc = __builtin_fmaf(wv.x, xv.x, acc);
-        acc = __builtin_fmaf(wv.y, xv.y, acc);
-        acc = __builtin_fmaf(wv.z, xv.z, acc);
-        acc = __builtin_fmaf(wv.w, xv.w, acc);
-      }
-      acc += b4[j];
-      const int64_t i = (int64_t)row * P + j / 3;
-      const int c = j % 3;
-      if (c < 2) {
-        const float v = acc + pts[i * 2 + c];
-        reg[i * 3 + c] = v;
-        if (pts_next) pts_next[i * 2 + c] = v;
-      } else {
-        reg[i * 3 + 2] = tanhf(acc) * 3.14159265358979323846f;
-      }
-    }
-  }
-}
-
-bool launch_reg_mlp(const float* x, int64_t ldx, const float* w0, const float* b0, const float* w2, const float* b2,
-                    const float* w4, const float* b4, int nin, int nhid, int nout, const float* pts, float* reg,
-                    float* pts_next, int rows, int P, hipStream_t st) {
-  if (nin != 256 || nhid != 256 || nout != P * 3 || kRB * nout > 256 || ldx % 4 || !b4 ||
-      (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w0) | reinterpret_cast<uintptr_t>(w2) |
-       reinterpret_cast<uintptr_t>(w4)) % 16)
-    return false;
-  if (rows == 0) return true;
-  hipLaunchKernelGGL(reg_mlp_kernel, dim3((rows + kRB - 1) / kRB), dim3(256), 0, st, x, ldx, w0, b0, w2, b2, w4, b4,
-                     pts, reg, pts_next, rows, P);
-  DD_HIP_CHECK(hipGetLastError());
-  return true;
-}
 
 // ---------------------------------------------------------------- DDIM step (eta = 0), diffusers semantics
 struct StepCoef {

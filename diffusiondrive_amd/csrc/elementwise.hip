@@ -202,110 +202,6 @@ __device__ inline float wave_sum(float v) {
   return v;
 }
 
-// ---------------------------------------------------------------- fused bev_proj tail (transfuser_model_v2.py:123-140)
-// cross_bev = LN(ReLU(W[:, 256:] p3 + b + bilinear(W[:, :256] keyval))) for one 64-pixel BEV row per
-// workgroup: the 64-channel p3 half of the 320 -> 256 projection on the VALU (thread j = output
-// channel j, its 64 fp32 weights in registers, p3 pixels as LDS broadcasts), the bilinear upsample of
-// the 8 x 8 keyval projection from two LDS source rows (upsample_bilinear2d arithmetic, bl_index),
-// ReLU, then LayerNorm(256) per pixel with one wave per 16 pixels (two-pass mean / variance as
-// layernorm_v4). Replaces the upsample (268 MB written), the K = 64 GEMM (reads it back) and the LN
-// pass (536 MB) with one write of cross_bev.
-__global__ __launch_bounds__(256) void bevproj_fused_kernel(const float* __restrict__ p3, int64_t p3_sn,
-                                                            int64_t p3_sh, int64_t p3_sw, const float* __restrict__ kvp,
-                                                            int Hk, int Wk, const float* __restrict__ w, int ldw,
-                                                            const float* __restrict__ bias,
-                                                            const float* __restrict__ g,
-                                                            const float* __restrict__ be, float* __restrict__ out,
-                                                            int H, float rh, float rw) {
-  constexpr int C = 256, KP = 64, NPX = 64;
-  __shared__ __attribute__((aligned(16))) float sm[NPX * C];  // phase 1: p3 row + 2 keyval rows; phase 2: tile
-  float* ps = sm;
-  float* kvs = sm + NPX * KP;
-  const int y = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const float* prow = p3 + (int64_t)b * p3_sn + (int64_t)y * p3_sh;
-  for (int i = tid; i < NPX * KP / 4; i += 256) {
-    const int px = i >> 4, c4 = (i & 15) * 4;
-    *reinterpret_cast<float4*>(ps + px * KP + c4) = *reinterpret_cast<const float4*>(prow + (int64_t)px * p3_sw + c4);
-  }
-  int y0, y1;
-  float ly0, ly1;
-  bl_index(y, rh, Hk, y0, y1, ly0, ly1);
-  const int nrow4 = Wk * C / 4;
-  for (int i = tid; i < 2 * nrow4; i += 256) {
-    const int r = i / nrow4, rem = i - r * nrow4;
-    const int yy = r ? y1 : y0;
-    *reinterpret_cast<float4*>(kvs + r * Wk * C + rem * 4) =
-        *reinterpret_cast<const float4*>(kvp + ((int64_t)(b * Hk + yy) * Wk) * C + rem * 4);
-  }
-  const int j = tid;
-  float wr[KP];
-#pragma unroll
-  for (int k4 = 0; k4 < KP / 4; ++k4) {
-    const float4 v = *reinterpret_cast<const float4*>(w + (int64_t)j * ldw + 4 * k4);
-    wr[4 * k4 + 0] = v.x;
-    wr[4 * k4 + 1] = v.y;
-    wr[4 * k4 + 2] = v.z;
-    wr[4 * k4 + 3] = v.w;
-  }
-  const float bj = bias[j];
-  __syncthreads();
-  float val[NPX];
-#pragma unroll
-  for (int px = 0; px < NPX; ++px) {
-    float acc = 0.f;
-#pragma unroll
-    for (int k4 = 0; k4 < KP / 4; ++k4) {
-      const float4 xv = *reinterpret_cast<const float4*>(ps + px * KP + 4 * k4);
-      acc = __builtin_fmaf(wr[4 * k4 + 0], xv.x, acc);
-      acc = __builtin_fmaf(wr[4 * k4 + 1], xv.y, acc);
-      acc = __builtin_fmaf(wr[4 * k4 + 2], xv.z, acc);
-      acc = __builtin_fmaf(wr[4 * k4 + 3], xv.w, acc);
-    }
-    int x0, x1;
-    float lx0, lx1;
-    bl_index(px, rw, Wk, x0, x1, lx0, lx1);
-    const float up = ly0 * (lx0 * kvs[x0 * C + j] + lx1 * kvs[x1 * C + j]) +
-                     ly1 * (lx0 * kvs[(Wk + x0) * C + j] + lx1 * kvs[(Wk + x1) * C + j]);
-    const float v = (acc + bj) + up;
-    val[px] = fmaxf(v, 0.f);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int px = 0; px < NPX; ++px) sm[px * C + j] = val[px];
-  __syncthreads();
-  const int wv = tid >> 6, lane = tid & 63;
-  const float4 gg = *reinterpret_cast<const float4*>(g + lane * 4);
-  const float4 bb = *reinterpret_cast<const float4*>(be + lane * 4);
-  for (int i = 0; i < NPX / 4; ++i) {
-    const int px = wv * (NPX / 4) + i;
-    const float4 v = *reinterpret_cast<const float4*>(sm + px * C + lane * 4);
-    const float mean = wave_sum((v.x + v.y) + (v.z + v.w)) / (float)C;
-    const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
-    const float q = (dx * dx + dy * dy) + (dz * dz + dw * dw);
-    const float rstd = rsqrtf(wave_sum(q) / (float)C + 1e-5f);
-    float4 o;
-    o.x = dx * rstd * gg.x + bb.x;
-    o.y = dy * rstd * gg.y + bb.y;
-    o.z = dz * rstd * gg.z + bb.z;
-    o.w = dw * rstd * gg.w + bb.w;
-    *reinterpret_cast<float4*>(out + ((int64_t)(b * H + y) * NPX + px) * C + lane * 4) = o;
-  }
-}
-
-bool launch_bevproj_fused(const float* p3, int64_t p3_sn, int64_t p3_sh, int64_t p3_sw, int Kp3, const float* kvp,
-                          int Hk, int Wk, const float* w, int ldw, const float* bias, const float* g, const float* be,
-                          float* out, int B, int H, int W, int C, hipStream_t st) {
-  if (C != 256 || Kp3 != 64 || W != 64 || Wk > 8 || Hk < 1 || Wk < 1 || B > 65535 || ldw % 4 || p3_sw % 4 ||
-      p3_sh % 4 || p3_sn % 4 || !bias || !g || !be ||
-      (reinterpret_cast<uintptr_t>(p3) | reinterpret_cast<uintptr_t>(kvp) | reinterpret_cast<uintptr_t>(w) |
-       reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(be)) % 16)
-    return false;
-  if (B == 0 || H == 0) return true;
-  hipLaunchKernelGGL(bevproj_fused_kernel, dim3(H, B), dim3(256), 0, st, p3, p3_sn, p3_sh, p3_sw, kvp, Hk, Wk, w, ldw,
-                     bias, g, be, out, H, (float)Hk / H, (float)Wk / W);
-  DD_HIP_CHECK(hipGetLastError());
-  return true;
-}
 
 __device__ inline float wave_max(float v) {
 #pragma unroll

@@ -33,6 +33,8 @@ extern "C" {
 
 const char* dd_op_last_error(void) { return g_op_err.c_str(); }
 
+const char* dd_op_last_kernel(void) { return last_conv_config(); }
+
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias, const float* res,
                  float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {
   return op_guard([&] {

@@ -59,8 +59,6 @@ struct DiffLayerW {
   LNp n1, n2, n3;
   Lin c0, c3, c6, r0, r2, r4;
   LNp c2, c5;
-  // reg-branch weights k-blocked for the fused VALU kernel: [nin / 4][nout][4] (launch_reg_mlp)
-  size_t r0_kb = kNone, r2_kb = kNone, r4_kb = kNone;
 };
 
 struct KStat {
@@ -131,14 +129,6 @@ class Model {
   bool value_dedup = true;
   // bev_proj's keyval half at 8 x 8 before the upsample (DDMI_BEVPROJ_LOWRES=0: concat at 64 x 64)
   bool bevproj_lowres = true;
-  // ... and its p3 half + upsample + ReLU + LN as one VALU pass (DDMI_BEVPROJ_FUSED=1). Off: parity green, but
-  // the first form takes ~0.33 ms, the same as the upsample + K = 64 GEMM + LN it replaces (4186/4169 vs
-  // 4254/4148 scenes/s, same box)
-  bool bevproj_fused = false;
-  // reg branch + finalize as one VALU kernel (DDMI_REG_FUSED=1). Off: measured in the B = 64 graph it takes
-  // ~31 us per layer against ~43 us for the three GEMMs + finalize, but the wall did not move (4150/4159 vs
-  // 4158/4189 scenes/s, same box) - the per-layer serial chain is bound by the k4 load latency it exposes
-  bool reg_fused = false;  // ... each distinct tap pixel of a scene once (DDMI_VALUE_DEDUP=0: every tap)
   // graph cache keyed by the forward's shape signature and the buffer generation
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
@@ -154,28 +144,15 @@ class Model {
     build(bx);
     ar.upload();
     decoder_init_constants();
-    // DDMI_SIDE_PRIO / DDMI_MAIN_PRIO = 1: that stream at the device's greatest priority. Measured
-    // (B = 64 bench graph): 4092 scenes/s default, 3950 side-high, 3968 main-high; both streams
-    // created explicitly at the LEAST priority dropped to 2725 - keep the default-priority streams.
-    int prio_least = 0, prio_greatest = 0;
-    DD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-    (void)prio_least;
-    auto make_stream = [&](hipStream_t* s, const char* env) {
-      const char* e = getenv(env);
-      if (e && atoi(e) != 0)
-        DD_HIP_CHECK(hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio_greatest));
-      else
-        DD_HIP_CHECK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-    };
-    make_stream(&st_main, "DDMI_MAIN_PRIO");
-    make_stream(&st_side, "DDMI_SIDE_PRIO");
+    // default-priority streams: either one at the device's greatest priority measured 3-3.5 % slower
+    // in the B = 64 bench graph, both at the least priority 33 % slower
+    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_main, hipStreamNonBlocking));
+    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_side, hipStreamNonBlocking));
     st = st_main;
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BEVPROJ_LOWRES")) bevproj_lowres = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_BEVPROJ_FUSED")) bevproj_fused = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_REG_FUSED")) reg_fused = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -279,18 +256,6 @@ class Model {
     return l;
   }
 
-  // W [nout][nin] -> [nin / 4][nout][4]: output j's 4 consecutive k at (k4 * nout + j) * 4, so a wave whose
-  // lanes are consecutive outputs reads 16 B per lane from one contiguous 1 KB segment
-  size_t prep_kblocked(const BlobIndex& bx, const std::string& name, int nout, int nin) {
-    if (nin % 4) throw std::runtime_error("prep_kblocked: nin % 4 != 0 for " + name);
-    const HostTensor& w = bx.get(name, {nout, nin});
-    std::vector<float> t((size_t)nout * nin);
-    for (int k4 = 0; k4 < nin / 4; ++k4)
-      for (int j = 0; j < nout; ++j)
-        for (int c = 0; c < 4; ++c) t[((size_t)k4 * nout + j) * 4 + c] = w.data[(size_t)j * nin + 4 * k4 + c];
-    return ar.add(t);
-  }
-
   void build(const BlobIndex& bx) {
     if (cfg.lidar_channels < 1 || cfg.lidar_channels > 4) throw std::invalid_argument("lidar_channels must be 1..4");
     build_trunk(bx, "_backbone.image_encoder", cfg.image_arch, 3, img);
@@ -386,9 +351,6 @@ class Model {
       w.r0 = prep_linear(bx, ar, t + ".plan_reg_branch.0", d, d);
       w.r2 = prep_linear(bx, ar, t + ".plan_reg_branch.2", d, d);
       w.r4 = prep_linear(bx, ar, t + ".plan_reg_branch.4", P * 3, d);
-      w.r0_kb = prep_kblocked(bx, t + ".plan_reg_branch.0.weight", d, d);
-      w.r2_kb = prep_kblocked(bx, t + ".plan_reg_branch.2.weight", d, d);
-      w.r4_kb = prep_kblocked(bx, t + ".plan_reg_branch.4.weight", P * 3, d);
       dl.push_back(w);
     }
     bevproj = prep_linear(bx, ar, "bev_proj.0", d, 320);
@@ -912,14 +874,7 @@ class Model {
       // on the 8 x 8 tokens and is upsampled into cross_bev, which the p3 half (K = 64) then adds to in place
       float* kvp = buf("kv_proj", (size_t)B * 64 * d);
       gemm_slice(bevproj, 0, d, false, KV, (int64_t)65 * d, d, B, 64, kvp, (int64_t)64 * d, d, false, nullptr, 0, 0);
-      bool fused = false;
-      if (bevproj_fused)  // p3 half + upsample + ReLU + LN in one VALU pass
-        launch("layernorm", 2.0 * MB * d * (CC - d), [&] {
-          fused = launch_bevproj_fused(cross_in + d, (int64_t)HB * WB * CC, (int64_t)WB * CC, CC, CC - d, kvp, 8, 8,
-                                       W(bevproj.w) + d, CC, W(bevproj.b), W(bevproj_ln.g), W(bevproj_ln.b), cross, B,
-                                       HB, WB, d, st);
-        });
-      if (!fused) {
+      {
         View4 a{kvp, (int64_t)64 * d, (int64_t)8 * d, d, 1};
         View4 o{cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, 1};
         launch("bilinear", 0, [&] { launch_bilinear(a, B, 8, 8, d, o, HB, WB, 8.0f / HB, 8.0f / WB, 0, st); });
@@ -951,13 +906,9 @@ class Model {
     }
     // the tf decoder branch is joined only where the trajectory head first reads its output (the
     // agent cross-attention of step 0 / layer 0): the trajectory embedding, anchor encoder, BEV
-    // sampling (and its gathered value rows) of that layer run beside the tf decoder's tail
+    // sampling (and its gathered value rows) of that layer run beside the tf decoder's tail (joining
+    // before the trajectory head measured 1.4 % slower)
     bool tf_pending = true;
-    static const bool join_early = getenv("DDMI_TF_JOIN_EARLY") && atoi(getenv("DDMI_TF_JOIN_EARLY")) != 0;
-    if (join_early) {
-      join();
-      tf_pending = false;
-    }
     const float* agents = q + d;   // rows 1..30
 
     // ---- optional heads (off the waypoint path), on the side stream beside the trajectory head
@@ -1126,21 +1077,10 @@ class Model {
         });
         float* reg = buf("reg" + sfx, (size_t)R * P * 3);
         float* nxt = (l == 0) ? pts2 : nullptr;
-        bool fused = false;
-        if (reg_fused) {
-          const double fl = 2.0 * R * ((double)w.r0.nout * w.r0.nin + (double)w.r2.nout * w.r2.nin +
-                                       (double)w.r4.nout * w.r4.nin);
-          launch("misc", fl, [&] {
-            fused = launch_reg_mlp(x2, d, W(w.r0_kb), W(w.r0.b), W(w.r2_kb), W(w.r2.b), W(w.r4_kb), W(w.r4.b), w.r0.nin,
-                                   w.r0.nout, w.r4.nout, cur, reg, nxt, R, P, st);
-          });
-        }
-        if (!fused) {
-          gemm(w.r0, x2, d, R, r1, d, true);
-          gemm(w.r2, r1, d, R, r2, d, true);
-          gemm(w.r4, r2, d, R, rr, P * 3);
-          launch("misc", 0, [&] { launch_reg_finalize(rr, cur, reg, nxt, R, P, st); });
-        }
+        gemm(w.r0, x2, d, R, r1, d, true);
+        gemm(w.r2, r1, d, R, r2, d, true);
+        gemm(w.r4, r2, d, R, rr, P * 3);
+        launch("misc", 0, [&] { launch_reg_finalize(rr, cur, reg, nxt, R, P, st); });
         cur = pts2;
         reg_last = reg;
         cls_last = cls;

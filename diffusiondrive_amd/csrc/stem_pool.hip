@@ -199,10 +199,9 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
 }  // namespace
 
 // Returns false when the conv is not a 7x7 / s2 / p3, Cin 4, Cout 64 f16x3 stem on a contiguous NHWC4
-// input (the caller then runs the conv and the pool separately). DDMI_STEM_POOL=0 disables it.
+// input (the caller then runs the conv and the pool separately).
 bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStream_t st) {
-  static const int on = getenv("DDMI_STEM_POOL") ? atoi(getenv("DDMI_STEM_POOL")) : 1;
-  if (!on || !a.wh || !a.wl || a.prec != 0 || !a.wsinv) return false;
+  if (!a.wh || !a.wl || a.prec != 0 || !a.wsinv) return false;
   if (a.KH != 7 || a.KW != 7 || a.stride != 2 || a.pad != 3 || a.Cin != 4 || a.Cout != 64 || a.batch != 1 || a.res ||
       !a.relu)
     return false;

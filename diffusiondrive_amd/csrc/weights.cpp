@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 
 namespace ddmi {
@@ -18,14 +19,19 @@ BlobIndex::BlobIndex(const void* blob, size_t bytes) {
   const uint8_t* p = static_cast<const uint8_t*>(blob);
   const uint8_t* end = p + bytes;
   auto need = [&](size_t n) {
-    if ((size_t)(end - p) < n) throw std::invalid_argument("weight blob truncated");
+    if (p > end || (size_t)(end - p) < n) throw std::invalid_argument("weight blob truncated");
+  };
+  // advance p to the next 16-byte boundary of the blob, never past its end
+  auto align16 = [&]() {
+    const size_t off = ((size_t)(p - static_cast<const uint8_t*>(blob)) + 15) & ~size_t(15);
+    if (off > bytes) throw std::invalid_argument("weight blob truncated");
+    p = static_cast<const uint8_t*>(blob) + off;
   };
   need(8);
   if (std::memcmp(p, "DDW1", 4) != 0) throw std::invalid_argument("weight blob: bad magic (expected DDW1)");
   uint32_t count;
   std::memcpy(&count, p + 4, 4);
   p += 8;
-  const uint8_t* base = static_cast<const uint8_t*>(blob);
   for (uint32_t i = 0; i < count; ++i) {
     need(4);
     uint32_t nl;
@@ -47,6 +53,7 @@ BlobIndex::BlobIndex(const void* blob, size_t bytes) {
       std::memcpy(&v, p, 8);
       p += 8;
       if (v < 0) throw std::invalid_argument("weight blob: negative dim for " + name);
+      if (v > 0 && numel > (SIZE_MAX / 4) / (size_t)v) throw std::invalid_argument("weight blob: tensor too large: " + name);
       t.shape.push_back(v);
       numel *= (size_t)v;
     }
@@ -55,16 +62,12 @@ BlobIndex::BlobIndex(const void* blob, size_t bytes) {
     std::memcpy(&dtype, p, 4);
     p += 4;
     if (dtype != 0) throw std::invalid_argument("weight blob: unsupported dtype for " + name);
-    size_t off = (size_t)(p - base);
-    off = (off + 15) & ~size_t(15);
-    p = base + off;
+    align16();
     need(numel * 4);
     t.data = reinterpret_cast<const float*>(p);
     t.numel = numel;
     p += numel * 4;
-    off = (size_t)(p - base);
-    off = (off + 15) & ~size_t(15);
-    p = base + off;
+    align16();
     map_[name] = t;
   }
 }

@@ -142,6 +142,14 @@ class DiffusionDriveModel:
         return out
 
     def _forward(self, features, noise, steps, heads, modes, stream) -> Dict[str, torch.Tensor]:
+        # stage inputs and allocate outputs on the stream the forward is ordered after, so the caching
+        # allocator ties their lifetime to it (the handle's stream waits on that stream and hands back to it)
+        dev = torch.device(f"cuda:{self.device}")
+        s = stream or torch.cuda.current_stream(dev)
+        with torch.cuda.stream(s):
+            return self._forward_on(features, noise, steps, heads, modes, s)
+
+    def _forward_on(self, features, noise, steps, heads, modes, s) -> Dict[str, torch.Tensor]:
         cfg = self.config
         cam = features["camera_feature"]
         out_device = cam.device if isinstance(cam, torch.Tensor) else torch.device("cpu")
@@ -180,7 +188,6 @@ class DiffusionDriveModel:
             outs.bev_semantic_map = res["bev_semantic_map"].data_ptr()
             outs.agent_states = res["agent_states"].data_ptr()
             outs.agent_labels = res["agent_labels"].data_ptr()
-        s = stream or torch.cuda.current_stream(dev)
         _lib.check(self.lib.dd_forward_ex(self.handle, cam.data_ptr(), lid.data_ptr(), st.data_ptr(), nz.data_ptr(),
                                           B, int(steps or cfg.denoise_steps), ctypes.byref(outs),
                                           s.cuda_stream), self.lib)

@@ -144,6 +144,9 @@ int dd_build_lidar(const float* xyz, const int64_t* offsets, int B, int channels
 /* ---- single-op entry points (parity tests of individual kernels) ---------------------------- */
 /* Last error message of a dd_op_* call on the calling thread. */
 const char* dd_op_last_error(void);
+/* Kernel and tile configuration of the calling thread's last conv / GEMM launch (dd_op_* or forward), e.g.
+ * "conv_x6<8,32,128,4,2>": lets tests prove which route a shape took. */
+const char* dd_op_last_kernel(void);
 /* NHWC conv: in (B,H,W,Cin), wgt (Cout,KH,KW,Cin), optional bias (Cout), res (B,Ho,Wo,Cout). */
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
                  const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream);

@@ -1,0 +1,46 @@
+"""CPU tests of bench.py's multi-rank launcher (the path the 1/2/4/8-GPU scaling run takes).
+
+``--cpu-plumbing`` swaps the forward for a stand-in step so the launcher, the gloo all_gather of
+ScenePlanner, the barrier / max-over-ranks timing and the rank-0 JSON run here without a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None, timeout=240):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          env=e, timeout=timeout, cwd=ROOT)
+
+
+def test_gpus2_launches_two_ranks():
+    r = _run(["--gpus", "2", "--cpu-plumbing", "--steps", "3", "--warmup", "1", "--batch", "4"])
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2
+    assert j["config"]["global_batch"] == 8
+    assert j["config"]["gathered_rows"] == 8
+    assert j["config"]["ranks_seen"] == [0, 1]
+    assert j["value"] > 0 and j["scaling"] == "weak"
+
+
+def test_gpus_must_match_world_size():
+    r = _run(["--gpus", "1", "--cpu-plumbing", "--steps", "1", "--warmup", "0"],
+             env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "disagrees" in r.stderr
+
+
+def test_single_rank_plumbing():
+    r = _run(["--cpu-plumbing", "--steps", "2", "--warmup", "0", "--batch", "2"])
+    assert r.returncode == 0, r.stderr
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["n_gpus"] == 1 and j["config"]["global_batch"] == 2

@@ -126,6 +126,40 @@ def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     close(out.permute(0, 3, 1, 2), ref, 3e-2)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p,relu,res,route", [
+    # the batch-dependent routes the B = 64 benchmark forward takes (bench.py's workload)
+    (64, 8, 32, 512, 512, 3, 1, 1, True, True, "conv_x6<8,32,128,4,2>"),     # image layer4 (256 WGs of BN 128)
+    (64, 32, 128, 128, 128, 3, 1, 1, True, True, "conv_x6<16,16,128,4,2>"),  # image layer2 3x3
+    (64, 64, 256, 64, 64, 3, 1, 1, True, True, "conv_x6<16,16,64,4,1>"),     # image layer1 (4-wave, 2 WG / CU)
+    (64, 64, 256, 64, 128, 3, 2, 1, True, False, "conv_x5<256,128>"),        # image layer2 entry, 3x3 / s2
+    (64, 32, 128, 128, 256, 3, 2, 1, True, False, "conv_x5<256,256>"),       # image layer3 entry, 3x3 / s2
+    (1, 160, 128, 512, 2048, 1, 1, 0, True, False, "conv_x5<256,256>"),      # GPT MLP-up at C = 512 (M = 20480)
+    (64, 8, 8, 512, 512, 3, 1, 1, True, True, "conv_x3<64,64,f16x3>"),       # LiDAR layer4 (8 x 8 maps)
+])
+def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, route):
+    """f16x3 conv at the B = 64 forward's shapes: the dispatcher must take the named kernel / tile
+    configuration (dd_op_last_kernel) and match PyTorch-CPU fp64 to 3e-5 of max|ref|."""
+    x = rnd(B, Cin, H, W, seed=61)
+    w = rnd(Cout, Cin, k, k, seed=62, scale=1.0 / np.sqrt(Cin * k * k))
+    b = rnd(Cout, seed=63)
+    ref = F.conv2d(x.double(), w.double(), b.double(), s, p)
+    r = rnd(*ref.shape, seed=64) if res else None
+    if res:
+        ref = ref + r.double()
+    if relu:
+        ref = F.relu(ref)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win, bin_ = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b)
+    rin = g(r.permute(0, 2, 3, 1)) if res else None
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(),
+                           rin.data_ptr() if res else None, out.data_ptr(), Cout, k, k, s, p, int(relu), 0,
+                           flags.data_ptr(), None), gpu)
+    assert gpu.dd_op_last_kernel().decode() == route
+    close(out.permute(0, 3, 1, 2), ref, 3e-5)
+    assert int(flags.item()) == 0
+
+
 def test_conv2d_f16x3_flags_overflow(gpu):
     """An activation beyond the fp16 range must raise DD_NUM_F16_OVERFLOW_BIT (never pass silently)."""
     x = rnd(1, 32, 8, 8, seed=15)

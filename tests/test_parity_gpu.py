@@ -18,6 +18,8 @@ pytestmark = pytest.mark.gpu
 
 WAYPOINT_L2_TOL = 1e-4
 HEADING_TOL = 1e-4
+MODE_TOL = 1e-4    # absolute, on every per-(step, layer) poses_reg (m / rad) and poses_cls (logit)
+AGENT_TOL = 5e-4   # absolute, agent_states (m / rad; x, y are tanh * 32, so 1e-5 relative = 3e-4 m) and labels
 TAP_TOL = 2e-5  # relative to max(1, |sample|max) on intermediates
 
 
@@ -83,7 +85,7 @@ def test_forward_matches_reference_goldens(gpu_model, path, mode):
     assert l2 <= WAYPOINT_L2_TOL, f"waypoint L2 {l2:.3e} > {WAYPOINT_L2_TOL}"
     assert hd <= HEADING_TOL
     for k, v in errs.items():
-        assert v <= 1e-4 * (1 + (np.abs(g[k]).max() if k in g else 0)), (k, v)
+        assert v <= (AGENT_TOL if k.startswith("agent") else MODE_TOL), (k, v)
     for k, (e, cs) in tap_errs.items():
         assert e <= TAP_TOL and cs <= TAP_TOL, (k, e, cs)
 
@@ -239,55 +241,3 @@ def test_gathered_value_rows_match_dense_map(gpu_model):
     ref = dense[rows[used]]
     err = np.abs(vals[used] - ref).max() / max(1.0, np.abs(ref).max())
     assert err <= TAP_TOL, err
-
-
-def test_fused_reg_branch_matches_gemm_path(gpu_model, seeded_sd, monkeypatch):
-    """DDMI_REG_FUSED=1 (reg branch Linear-ReLU-Linear-ReLU-Linear + finalize, transfuser_model_v2.py:208-256,
-    375-382, as one VALU kernel over k-blocked fp32 weights) against the default GEMM path on the same
-    inputs: every per-(step, layer) reg output within the 1e-4 bar."""
-    from diffusiondrive_amd.model import DiffusionDriveModel
-    from diffusiondrive_amd.weights import synthetic_inputs
-    B = 4
-    inp = synthetic_inputs(B, 17)
-    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
-    nz = torch.from_numpy(inp["noise"])
-    gpu_model.set_gemm_mode("f16x3")
-    try:
-        ref_out = gpu_model.forward(feats, noise=nz)["trajectory"].numpy()
-        ref = {f"reg_s{s}l{l}": gpu_model.tap(f"reg_s{s}l{l}", (B, 20, 8, 3)).cpu().numpy()
-               for s in range(2) for l in range(2)}
-    finally:
-        gpu_model.set_gemm_mode("fp32")
-    monkeypatch.setenv("DDMI_REG_FUSED", "1")
-    monkeypatch.setenv("DDMI_GEMM", "f16x3")
-    m = DiffusionDriveModel(state_dict=seeded_sd, device=0)
-    out = m.forward(feats, noise=nz)["trajectory"].numpy()
-    for k, v in ref.items():
-        got = m.tap(k, (B, 20, 8, 3)).cpu().numpy()
-        assert np.abs(got - v).max() <= 1e-4 * (1 + np.abs(v).max()), (k, np.abs(got - v).max())
-    assert np.abs(out - ref_out).max() <= 1e-3
-
-
-def test_fused_bevproj_matches_default_path(gpu_model, seeded_sd, monkeypatch):
-    """DDMI_BEVPROJ_FUSED=1 (bev_proj's p3 half + bilinear upsample of the 8x8 keyval projection + ReLU +
-    LayerNorm in one VALU pass, transfuser_model_v2.py:123-140) against the default path: cross_bev and
-    the trajectories on the same inputs."""
-    from diffusiondrive_amd.model import DiffusionDriveModel
-    from diffusiondrive_amd.weights import synthetic_inputs
-    B = 2
-    inp = synthetic_inputs(B, 23)
-    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
-    nz = torch.from_numpy(inp["noise"])
-    gpu_model.set_gemm_mode("f16x3")
-    try:
-        ref_out = gpu_model.forward(feats, noise=nz)["trajectory"].numpy()
-        ref = gpu_model.tap("cross_bev", (B, 4096, 256)).double().cpu().numpy()
-    finally:
-        gpu_model.set_gemm_mode("fp32")
-    monkeypatch.setenv("DDMI_BEVPROJ_FUSED", "1")
-    monkeypatch.setenv("DDMI_GEMM", "f16x3")
-    m = DiffusionDriveModel(state_dict=seeded_sd, device=0)
-    out = m.forward(feats, noise=nz)["trajectory"].numpy()
-    got = m.tap("cross_bev", (B, 4096, 256)).double().cpu().numpy()
-    assert np.abs(got - ref).max() <= TAP_TOL * max(1.0, np.abs(ref).max())
-    assert np.abs(out - ref_out).max() <= 1e-3

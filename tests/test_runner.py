@@ -39,3 +39,31 @@ def test_runner_matches_per_token_compute_trajectory(gpu, seeded_sd):
         ref = agent.compute_trajectory(inputs[tok])
         l2 = float(np.sqrt(((got[tok].poses[:, :2].astype(np.float64) - ref.poses[:, :2]) ** 2).sum()))
         assert got[tok].poses.shape == (8, 3) and l2 <= 1e-4, (tok, l2)
+
+
+@pytest.mark.gpu
+def test_runner_matches_oracle_on_same_noise(gpu, seeded_sd):
+    """The batched runner (GPU features + batched forward) against the CPU oracle: oracle features
+    (oracle/features.py) and the oracle forward on the same per-scene noise the runner drew
+    (torch.manual_seed(9); one randn(b, 20, 8, 2) per batch == successive per-token draws)."""
+    from diffusiondrive_amd.agent import DiffusionDriveAgent
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.runner import BatchedTrajectoryRunner
+    from oracle.model import OracleModel
+    from test_agent import _oracle_features
+    cfg = TransfuserConfig()
+    agent = DiffusionDriveAgent(cfg, device=0)
+    agent.load_state_dict(seeded_sd)
+    toks = [f"t{i}" for i in range(3)]
+    inputs = {t: make_agent_input(300 + i, n_points=8000 + 500 * i) for i, t in enumerate(toks)}
+    torch.manual_seed(9)
+    got = BatchedTrajectoryRunner(agent, batch_size=2).run(toks, inputs.__getitem__)
+    torch.manual_seed(9)
+    noise = torch.cat([torch.randn(2, 20, 8, 2), torch.randn(1, 20, 8, 2)])  # the runner's two batches
+    f = [_oracle_features(inputs[t]) for t in toks]
+    cat = {k: torch.stack([x[k] for x in f]).numpy() for k in f[0]}
+    ref = OracleModel(seeded_sd).forward(cat["camera_feature"], cat["lidar_feature"], cat["status_feature"],
+                                         noise.numpy(), heads=False)["trajectory"].numpy()
+    for i, t in enumerate(toks):
+        l2 = float(np.sqrt(((got[t].poses[:, :2].astype(np.float64) - ref[i, :, :2]) ** 2).sum()))
+        assert l2 <= 1e-4, (t, l2)

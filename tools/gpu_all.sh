@@ -11,7 +11,7 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[$name] abnormal exit ($rc): stopping"; exit $rc; fi
   return $rc
 }
-step tests 900 python -u -m pytest tests -q -m gpu -x -rf --timeout 300 --timeout-method thread || exit 1
+step tests 900 python -u -m pytest tests -v -m gpu -x -rf --timeout 300 --timeout-method thread || exit 1
 step bench 600 python bench.py ${BENCH_ARGS:-}
 cd /tmp && export TMPDIR=/tmp
 # single-stream replays (DDMI_STREAMS=0) so per-kernel durations match bench.py's profiled replay; no fp32 leg
