@@ -498,7 +498,7 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
     g_last_conv = "conv_x6";
     return;
   }
-  if (a.prec == 0 && launch_conv_x5(a, M, K, st)) {
+  if (launch_conv_x5(a, M, K, st)) {
     g_last_conv = "conv_x5";
     return;
   }

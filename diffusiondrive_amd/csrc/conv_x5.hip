@@ -1,5 +1,5 @@
-// f16x3 implicit-GEMM conv / GEMM, LDS-DMA edition (the default f16x3 kernel; conv_x3.hip keeps
-// the register-staged variant and the bf16 mode).
+// f16x3 / bf16 implicit-GEMM conv / GEMM, LDS-DMA edition (the default kernel for grids that fill the
+// chip; conv_x3.hip keeps the register-staged variant for the rest).
 //
 // Same arithmetic as conv_x3.hip (fp32 operands split into fp16 hi + lo, products ah*bh + ah*bl +
 // al*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation; numerics in that file's header), different
@@ -39,6 +39,8 @@ typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 half2_v __attribute__((ext_vector_type(2)));
 typedef float float2_v __attribute__((ext_vector_type(2)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
 
 constexpr int KC = 32;                 // K chunk
 constexpr uint32_t kOOB5 = 0x80000000u;
@@ -83,9 +85,24 @@ __device__ inline void split8(const float4& p, const float4& q, half8_t& hi, hal
   }
 }
 
+// 8 fp32 -> bf16 fragment (RNE)
+__device__ inline bf16x8_t to_bf16x8(const float4& p, const float4& q) {
+  const float x[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+  bf16x8_t r;
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const bf16x2_v b = __builtin_convertvector((float2_v){x[e], x[e + 1]}, bf16x2_v);
+    r[e] = b.x;
+    r[e + 1] = b.y;
+  }
+  return r;
+}
+
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE, int NS>
+// PREC 0: f16x3; PREC 1: the bf16 mode (A converted to bf16 at fragment-read time, B = the bf16 weight
+// image, one v_mfma_f32_32x32x16_bf16 per MAC; the stage's second B image is not filled).
+template <int WM, int WN, int TM, int TN, int MODE, int NS, int PREC>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 (scalar tap walk, per-row tap masks); MODE 0: generic K.
@@ -94,13 +111,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   constexpr int BN = WN * TN * 32;
   constexpr int AB = BM * KC * 4;     // A stage bytes (fp32 rows of 128 B)
   constexpr int BB = BN * KC * 2;     // one B image (fp16 rows of 64 B)
-  constexpr int STAGE = AB + 2 * BB;
+  constexpr int STAGE = AB + (PREC ? 1 : 2) * BB;  // bf16: one B image (so one more stage fits)
   constexpr int A_IN = BM / 8 / NW;   // A DMA instructions per wave per chunk (8 rows x 128 B each)
   constexpr int B_IN = BN / 16 / NW;  // B DMA instructions per wave per chunk and image (16 rows x 64 B)
   static_assert(A_IN >= 1 && BM % (8 * NW) == 0, "A rows per wave");
   static_assert(B_IN >= 1 && BN % (16 * NW) == 0, "B rows per wave");
   static_assert(NS >= 2 && NS * STAGE <= 160 * 1024, "stages");
-  constexpr int DPC = A_IN + 2 * B_IN;  // DMA instructions per wave per chunk
+  constexpr int DPC = A_IN + (PREC ? 1 : 2) * B_IN;  // DMA instructions per wave per chunk
   __shared__ __attribute__((aligned(1024))) char lds[NS * STAGE];
   const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
 
@@ -208,7 +225,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
     for (int q = 0; q < B_IN; ++q) {
       const uint32_t off = (bok[q] && k0 + bkb[q] < Kp) ? boff[q] + (uint32_t)k0 * 2u : kOOB5;
       dma16(rwh, __builtin_amdgcn_readfirstlane(st + AB + (b_rbase + q * 16) * 64), off);
-      dma16(rwl, __builtin_amdgcn_readfirstlane(st + AB + BB + (b_rbase + q * 16) * 64), off);
+      if constexpr (PREC == 0) dma16(rwl, __builtin_amdgcn_readfirstlane(st + AB + BB + (b_rbase + q * 16) * 64), off);
     }
   };
 
@@ -253,6 +270,24 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
     issue(nxt, (kc + NS - 1) * KC);
     const char* st = lds + cur * STAGE;
     if (++cur == NS) cur = 0;
+    if constexpr (PREC == 1) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8_t ab[TM], bb[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bb[j] = *reinterpret_cast<const bf16x8_t*>(st + b_ro[s2][j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          ab[i] = to_bf16x8(*reinterpret_cast<const float4*>(st + a_ro[s2][i][0]),
+                            *reinterpret_cast<const float4*>(st + a_ro[s2][i][1]));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab[i], bb[j], acc[i][j], 0, 0, 0);
+      }
+      continue;
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       half8_t ah[TM], al[TM], bh[TN], bl[TN];
@@ -347,19 +382,29 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
-template <int WM, int WN, int TM, int TN, int NS>
-static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
+template <int WM, int WN, int TM, int TN, int NS, int PREC>
+static void launch_x5_one(const ConvArgs& a, int M, int K, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int ntm = (M + BM - 1) / BM;
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
-  static const std::string name = "conv_x5<" + std::to_string(BM) + "," + std::to_string(BN) + ">";
+  static const std::string name =
+      "conv_x5<" + std::to_string(BM) + "," + std::to_string(BN) + (PREC ? ",bf16>" : ">");
   set_last_conv_config(name.c_str());
   if (a.Cin % KC == 0 && a.KH * a.KW <= 32)
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS, PREC>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
+                       ntn);
   else
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS, PREC>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
+                       ntn);
   DD_HIP_CHECK(hipGetLastError());
+}
+template <int WM, int WN, int TM, int TN, int NS>
+static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
+  if (a.prec == 1)
+    launch_x5_one<WM, WN, TM, TN, NS + 1, 1>(a, M, K, st);  // the freed B image buys a stage
+  else
+    launch_x5_one<WM, WN, TM, TN, NS, 0>(a, M, K, st);
 }
 
 // Returns false when the shape is better served by conv_x3 (grids too small to fill the chip).
@@ -367,6 +412,7 @@ static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 // grids that fill the chip only at 256 x 128, and 128 x 128 tiles for the mid-size GEMMs, measured
 // slower than conv_x3 on the GPT shapes (tools/micro/gemm_x3_bench.py) and are not routed here.
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
+  if (a.prec != 0 && a.prec != 1) return false;
   const int64_t m256 = (M + 255) / 256;
   const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;
   if (a.Cout <= 64) {

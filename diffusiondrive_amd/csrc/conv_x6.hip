@@ -5,7 +5,8 @@
 //
 // Arithmetic: exactly conv_x3.hip's f16x3 (fp32 operand = fp16 hi + lo, products ah*bh + ah*bl +
 // al*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation; numerics and range in that file's header;
-// non-finite accumulators raise DD_NUM_F16_OVERFLOW).
+// non-finite accumulators raise DD_NUM_F16_OVERFLOW), or the bf16 mode's one bf16 product per MAC
+// (v_mfma_f32_32x32x16_bf16; PREC 1 below: 64-channel K chunks in the same LDS bytes).
 //
 // Why a direct kernel: the implicit GEMM (conv_x3 / conv_x5) fetches every input pixel once per
 // filter tap, 9x; with f16x3's 4 B per operand element that needs 21-53 B/clk per CU at full MFMA
@@ -45,6 +46,8 @@ typedef float x6f2 __attribute__((ext_vector_type(2)));
 typedef float x6f4 __attribute__((ext_vector_type(4)));
 typedef float x6f16 __attribute__((ext_vector_type(16)));
 typedef int x6i4 __attribute__((ext_vector_type(4)));
+typedef __bf16 x6b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 x6b2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t kOOB6 = 0x80000000u;
 
@@ -55,6 +58,9 @@ __device__ inline x6i4 rsrc6(const void* p) {
   r.y = (int)((uint32_t)(a >> 32) & 0xffffu);  // stride 0
   r.z = (int)kOOB6;                             // num_records: offsets >= 2^31 read as zero
   r.w = 0x00020000;
+  // wave-uniform by construction; readfirstlane keeps it in SGPRs for the "s" asm operands
+  r.x = __builtin_amdgcn_readfirstlane(r.x);
+  r.y = __builtin_amdgcn_readfirstlane(r.y);
   return r;
 }
 
@@ -94,6 +100,12 @@ __device__ inline void split4(const x6f4 v, uint2& hi, uint2& lo) {
   lo = make_uint2(__builtin_bit_cast(uint32_t, l01), __builtin_bit_cast(uint32_t, l23));
 }
 
+__device__ inline uint2 to_bf16x4(const x6f4 v) {  // RNE (v_cvt_pk_bf16_f32)
+  const x6b2 b01 = __builtin_convertvector((x6f2){v.x, v.y}, x6b2);
+  const x6b2 b23 = __builtin_convertvector((x6f2){v.z, v.w}, x6b2);
+  return make_uint2(__builtin_bit_cast(uint32_t, b01), __builtin_bit_cast(uint32_t, b23));
+}
+
 // Does a halo issue (at tap TA of some chunk) fall in the D steps before step t, i.e. after the B
 // DMAs of step t were issued (D steps earlier, ahead of that step's halo)? For the first chunk the
 // window stops at step 0 (the prologue issued chunk 0's halo before every B DMA).
@@ -113,7 +125,10 @@ constexpr bool halo_in_window(int t, int D, int TA, bool first) {
 // barrier that retires every wave's last read of the current one), so a 4-wave BN = 64 workgroup
 // fits twice per CU (66 KB of LDS) and one workgroup's prologue / epilogue runs beside the other's
 // MFMAs.
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
+// PREC 0: f16x3 (32-channel chunks; a halo pixel row / B slot holds the hi and lo fp16 images of them);
+// PREC 1: bf16 (64-channel chunks; the same bytes hold channels 0-31 and 32-63 of the chunk in bf16, and
+// each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
 __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks) {
   constexpr int NW = WM * WN, NT = 64 * NW;
@@ -130,7 +145,9 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   constexpr int BQ = BN / 16;               // DMA instructions per image per step
   constexpr int BPS = 2 * BQ / NW;          // per wave per step
   static_assert(BPS >= 1 && (2 * BQ) % NW == 0 && BQ % BPS == 0, "B DMA split over the waves");
-  constexpr int ALD = (HP * 8 + NT - 1) / NT;  // halo float4 loads per thread per chunk
+  constexpr int CH = PREC ? 64 : 32;           // input channels per K chunk
+  constexpr int QP = CH / 4;                   // float4 quads per halo pixel per chunk
+  constexpr int ALD = (HP * QP + NT - 1) / NT;  // halo float4 loads per thread per chunk
   constexpr int TA = 1;                        // tap step at which the next chunk's halo is issued
   constexpr int NHB = SH ? 1 : 2;          // halo buffers
   constexpr int B_OFF = NHB * ABYTES;
@@ -163,12 +180,12 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
 
   // ---- halo staging: thread element e = tid + NT i -> halo pixel e >> 3, channels 4 (e & 7) ..
   // hofs: element offset of (pixel, 4q) at chunk 0, or -1 (zero fill); hwad: LDS byte offset (in a
-  // halo buffer) of the hi 8 bytes, -1 = no write. Kept in registers for 8-wave workgroups (ALD <= 6),
-  // recomputed per use by 4-wave ones (ALD = 11), whose register file is the limit.
-  constexpr bool HKEEP = ALD <= 6;
+  // halo buffer) of the hi 8 bytes (bf16: of the quad's 8 bytes), -1 = no write. Kept in registers for
+  // 8-wave workgroups, recomputed per use by 4-wave ones (ALD = 11), whose register file is the limit.
+  constexpr bool HKEEP = NW == 8 && ALD <= 12;
   auto hofs_of = [&](int i) {
     const int e = tid + NT * i;
-    const int px = e >> 3, q = e & 7;
+    const int px = e / QP, q = e % QP;
     const int hy = px / P, hx = px - (px / P) * P;
     const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
     const bool in = px < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
@@ -176,9 +193,10 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   };
   auto hwad_of = [&](int i) {
     const int e = tid + NT * i;
-    const int px = e >> 3, q = e & 7;
+    const int px = e / QP, q = e % QP;
+    const int q7 = q & 7, half = q >> 3;  // bf16: quads 8..15 (channels 32..63) fill the second 64 B
     const int hx = px - (px / P) * P;
-    return px < HP ? px * 128 + ((((q >> 1) ^ (hx >> 1)) & 7) << 4) + ((q & 1) << 3) : -1;
+    return px < HP ? (px * 128 + ((((q7 >> 1) ^ (hx >> 1)) & 7) << 4) + ((q7 & 1) << 3)) ^ (half << 6) : -1;
   };
   int hofs[HKEEP ? ALD : 1], hwad[HKEEP ? ALD : 1];
   if constexpr (HKEEP) {
@@ -191,7 +209,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   x6f4 hr[ALD];
   auto halo_issue = [&](int c) {
     const bool cv = c < nchunks;
-    const int co = c * 32;
+    const int co = c * CH;
 #pragma unroll
     for (int i = 0; i < ALD; ++i) {
       const int ho = HKEEP ? hofs[HKEEP ? i : 0] : hofs_of(i);
@@ -208,10 +226,14 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     for (int i = 0; i < ALD; ++i) {
       const int hw = HKEEP ? hwad[HKEEP ? i : 0] : hwad_of(i);
       if (hw < 0) continue;
-      uint2 hi, lo;
-      split4(hr[i], hi, lo);
-      *reinterpret_cast<uint2*>(base + hw) = hi;
-      *reinterpret_cast<uint2*>(base + (hw ^ 64)) = lo;
+      if constexpr (PREC == 1) {
+        *reinterpret_cast<uint2*>(base + hw) = to_bf16x4(hr[i]);
+      } else {
+        uint2 hi, lo;
+        split4(hr[i], hi, lo);
+        *reinterpret_cast<uint2*>(base + hw) = hi;
+        *reinterpret_cast<uint2*>(base + (hw ^ 64)) = lo;
+      }
     }
   };
 
@@ -231,10 +253,12 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     brow[j] = rb;
   }
   const bool bimg_lo = (wave * BPS) / BQ == 1;
-  const x6i4 rwb = rsrc6(bimg_lo ? (const void*)a.wl : (const void*)a.wh);
+  // f16x3: the second image of a slot is the lo split image; bf16: channels 32..63 of the same image
+  const x6i4 rwb = rsrc6((bimg_lo && !PREC) ? (const void*)a.wl : (const void*)a.wh);
+  const uint32_t kb_lo = (PREC && bimg_lo) ? 64u : 0u;
   auto b_issue = [&](int slot, int tap, int c) {
     const bool cv = c < nchunks;
-    const uint32_t kb = (uint32_t)(tap * Cin + c * 32) * 2u;
+    const uint32_t kb = (uint32_t)(tap * Cin + c * CH) * 2u + kb_lo;
 #pragma unroll
     for (int j = 0; j < BPS; ++j) {
       const uint32_t dst = lds_u32 + B_OFF + slot * BSLOT + (bimg_lo ? BIMG : 0) + brow[j] * 64;
@@ -292,6 +316,21 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     }
   };
   auto mfma_frag = [&](const Frag& F) {
+    if constexpr (PREC == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(x6b8, F.ah[i]),
+                                                             __builtin_bit_cast(x6b8, F.bh[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(x6b8, F.al[i]),
+                                                             __builtin_bit_cast(x6b8, F.bl[j]), acc[i][j], 0, 0, 0);
+      return;
+    }
     // small terms first, the hi x hi term last (independent accumulators interleaved)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -450,24 +489,37 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
-static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
+static void launch_x6_one(const ConvArgs& a, hipStream_t st) {
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   const int n_sp = a.Nimg * tiles_x * tiles_y;
   const int ntn = (a.Cout + BN - 1) / BN;
   static const std::string name = "conv_x6<" + std::to_string(TH) + "," + std::to_string(TW) + "," +
-                                  std::to_string(BN) + "," + std::to_string(WM) + "," + std::to_string(WN) + ">";
+                                  std::to_string(BN) + "," + std::to_string(WM) + "," + std::to_string(WN) +
+                                  (PREC ? ",bf16>" : ">");
   set_last_conv_config(name.c_str());
-  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0, st,
-                     a, tiles_x, tiles_y, n_sp, ntn, a.Cin / 32);
+  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0,
+                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32));
   DD_HIP_CHECK(hipGetLastError());
 }
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
+static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
+  if constexpr (SH == 0) {
+    if (a.prec == 1) {
+      launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 1>(a, st);
+      return;
+    }
+  } else {
+    if (a.prec == 1) throw std::runtime_error("conv_x6: bf16 takes the 8-wave configurations");
+  }
+  launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
+}
 
-// Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 conv this kernel covers (the
+// Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 / bf16 conv this kernel covers (the
 // caller then takes conv_x5 / conv_x3).
 bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
-  if (a.prec != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || a.Cin % 32 != 0 || a.batch != 1 ||
-      a.b_kn)
+  if ((a.prec != 0 && a.prec != 1) || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 ||
+      a.Cin % (a.prec ? 64 : 32) != 0 || a.batch != 1 || a.b_kn)
     return false;
   if (a.Ho != a.H || a.Wo != a.W || a.Ho < 8) return false;
   // the epilogue moves 16-B channel quads
@@ -485,8 +537,9 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   const bool bn128 = a.Cout > 64 && n_sp * ((a.Cout + 127) / 128) >= 256;
   // BN = 64 with Cin <= 64 (2 K chunks per tile: prologue / epilogue-heavy): 4-wave workgroups
   // (wave tile 64 x 64) with one halo buffer, two per CU - 12 % faster on the 64-channel layers,
-  // 11 % slower at Cin = 256 (tools/micro/conv_bench)
-  const bool sh4 = a.Cin <= 64;
+  // 11 % slower at Cin = 256 (tools/micro/conv_bench). bf16 keeps the 8-wave form (its 64-channel halo
+  // chunk would double the 4-wave form's staging registers)
+  const bool sh4 = a.prec == 0 && a.Cin <= 64;
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   if (wide) {
     if (bn128) {

@@ -124,7 +124,13 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
 
 int dd_op_stem_pool_x3(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out,
                        unsigned* flags, void* stream) {
+  return dd_op_stem_pool(in, B, H, W, wgt, bias, out, 0, flags, stream);
+}
+
+int dd_op_stem_pool(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out, int prec,
+                    unsigned* flags, void* stream) {
   return op_guard([&] {
+    if (prec != 0 && prec != 1) throw std::invalid_argument("stem_pool: prec must be 0 (f16x3) or 1 (bf16)");
     const int Cin = 4, Cout = 64, K = 7 * 7 * Cin;
     std::vector<float> hw((size_t)Cout * K);
     DD_HIP_CHECK(hipStreamSynchronize(S(stream)));
@@ -151,8 +157,8 @@ int dd_op_stem_pool_x3(const float* in, int B, int H, int W, const float* wgt, c
     a.stride = 2;
     a.pad = 3;
     a.relu = 1;
-    a.prec = 0;
-    a.wh = reinterpret_cast<const uint16_t*>(ar.ptr(x.hi));
+    a.prec = prec;
+    a.wh = reinterpret_cast<const uint16_t*>(ar.ptr(prec ? x.b16 : x.hi));
     a.wl = reinterpret_cast<const uint16_t*>(ar.ptr(x.lo));
     a.wsinv = ar.ptr(x.sinv);
     a.ldh = x.ldh;

@@ -9,7 +9,8 @@
 //
 // Arithmetic: f16x3 as conv_x3.hip (fp32 operands split into fp16 hi + lo, products al*bh + ah*bl +
 // ah*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation, per-channel power-of-two weight scale undone
-// in the epilogue, non-finite accumulators raise DD_NUM_F16_OVERFLOW).
+// in the epilogue, non-finite accumulators raise DD_NUM_F16_OVERFLOW), or (PREC 1, the bf16 mode) one
+// bf16 product per MAC on v_mfma_f32_32x32x16_bf16 from the bf16 weight image.
 //  * GEMM view per tile: M = stem pixels (297 -> 10 tiles of 32), N = 64 channels (2 tiles),
 //    K = 7 kh x 8 kw x 4 ch = 224 (kw = 7 is a zero tap): 14 k16 steps, each = one kernel row kh and
 //    four consecutive taps = 4 consecutive input pixels of that row.
@@ -27,8 +28,6 @@
 //    loaded into registers while the current tile's MFMAs run.
 // Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.16 x recompute,
 // 224 / 196 K padding; HBM traffic = the input once (+ halo re-reads) + the pooled map.
-#include <cstdlib>
-
 #include "common.h"
 
 namespace ddmi {
@@ -39,6 +38,8 @@ typedef _Float16 sp_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 sp_h4 __attribute__((ext_vector_type(4)));
 typedef float sp_f4 __attribute__((ext_vector_type(4)));
 typedef float sp_f16 __attribute__((ext_vector_type(16)));
+typedef __bf16 sp_b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 sp_b4 __attribute__((ext_vector_type(4)));
 
 constexpr int PH = 4, PW = 16;                     // pooled outputs per tile
 constexpr int SH = 2 * PH + 1, SW = 2 * PW + 1;    // stem pixels per tile (9 x 33)
@@ -60,6 +61,7 @@ __device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
   lo = __builtin_convertvector(r, sp_h4);
 }
 
+template <int PREC>
 __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__ in, int H, int W, int Hs, int Ws,
                                                        int Hp, int Wp, const uint16_t* __restrict__ wh,
                                                        const uint16_t* __restrict__ wl, int ldh,
@@ -83,11 +85,11 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     const int kh = s >> 1, kw0 = 4 * (s & 1) + 2 * hl;
     const int64_t o = (int64_t)co * ldh + kh * 28 + kw0 * 4;
     const uint2 h0 = *reinterpret_cast<const uint2*>(wh + o);
-    const uint2 l0 = *reinterpret_cast<const uint2*>(wl + o);
+    const uint2 l0 = PREC ? make_uint2(0u, 0u) : *reinterpret_cast<const uint2*>(wl + o);
     uint2 h1 = make_uint2(0u, 0u), l1 = make_uint2(0u, 0u);
     if (kw0 + 1 < 7) {
       h1 = *reinterpret_cast<const uint2*>(wh + o + 4);
-      l1 = *reinterpret_cast<const uint2*>(wl + o + 4);
+      if (!PREC) l1 = *reinterpret_cast<const uint2*>(wl + o + 4);
     }
     const uint4 hv = make_uint4(h0.x, h0.y, h1.x, h1.y), lv = make_uint4(l0.x, l0.y, l1.x, l1.y);
     bh[s] = __builtin_bit_cast(sp_h8, hv);
@@ -124,10 +126,14 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       const int e = tid + NT * i;
       if (e < IH * IW) {
         const int r = e / IW, c = e - (e / IW) * IW;
-        sp_h4 hi, lo;
-        sp_split4(pre[i], hi, lo);
-        *reinterpret_cast<sp_h4*>(in_hi + (r * IP + c) * 8) = hi;
-        *reinterpret_cast<sp_h4*>(in_lo + (r * IP + c) * 8) = lo;
+        if constexpr (PREC == 1) {
+          *reinterpret_cast<sp_b4*>(in_hi + (r * IP + c) * 8) = __builtin_convertvector(pre[i], sp_b4);
+        } else {
+          sp_h4 hi, lo;
+          sp_split4(pre[i], hi, lo);
+          *reinterpret_cast<sp_h4*>(in_hi + (r * IP + c) * 8) = hi;
+          *reinterpret_cast<sp_h4*>(in_lo + (r * IP + c) * 8) = lo;
+        }
       }
     }
   };
@@ -154,10 +160,15 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       for (int s = 0; s < KS; ++s) {
         const int off = (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
         const sp_h8 ah = *reinterpret_cast<const sp_h8*>(in_hi + off);
-        const sp_h8 al = *reinterpret_cast<const sp_h8*>(in_lo + off);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+        if constexpr (PREC == 1) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_b8, ah), __builtin_bit_cast(sp_b8, bh[s]),
+                                                        acc, 0, 0, 0);
+        } else {
+          const sp_h8 al = *reinterpret_cast<const sp_h8*>(in_lo + off);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+        }
       }
       // C/D layout: column (channel) li, row (pixel) (r & 3) + 8 (r >> 2) + 4 hl
 #pragma unroll
@@ -198,10 +209,10 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
 
 }  // namespace
 
-// Returns false when the conv is not a 7x7 / s2 / p3, Cin 4, Cout 64 f16x3 stem on a contiguous NHWC4
-// input (the caller then runs the conv and the pool separately).
+// Returns false when the conv is not a 7x7 / s2 / p3, Cin 4, Cout 64 f16x3 / bf16 stem on a contiguous
+// NHWC4 input (the caller then runs the conv and the pool separately).
 bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStream_t st) {
-  if (!a.wh || !a.wl || a.prec != 0 || !a.wsinv) return false;
+  if (!a.wh || (a.prec == 0 && !a.wl) || (a.prec != 0 && a.prec != 1) || !a.wsinv) return false;
   if (a.KH != 7 || a.KW != 7 || a.stride != 2 || a.pad != 3 || a.Cin != 4 || a.Cout != 64 || a.batch != 1 || a.res ||
       !a.relu)
     return false;
@@ -210,7 +221,7 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   const int Hs = a.Ho, Ws = a.Wo;
   if (Hp != (Hs + 2 - 3) / 2 + 1 || Wp != (Ws + 2 - 3) / 2 + 1) return false;
   if ((reinterpret_cast<uintptr_t>(a.in) & 15) || (reinterpret_cast<uintptr_t>(pool_out) & 15) ||
-      (reinterpret_cast<uintptr_t>(a.wh) & 7) || (reinterpret_cast<uintptr_t>(a.wl) & 7))
+      (reinterpret_cast<uintptr_t>(a.wh) & 7) || (a.prec == 0 && (reinterpret_cast<uintptr_t>(a.wl) & 7)))
     return false;
   const int tiles_x = (Wp + PW - 1) / PW, tiles_y = (Hp + PH - 1) / PH;
   const int64_t nt64 = (int64_t)a.Nimg * tiles_x * tiles_y;
@@ -220,14 +231,21 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   DD_HIP_CHECK(hipGetDevice(&dev));
   DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int grid = ntiles < cus ? ntiles : cus;
-  static bool attr = false;
-  if (!attr) {
-    DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    attr = true;
-  }
-  hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, a.H, a.W, Hs, Ws, Hp, Wp, a.wh,
-                     a.wl, (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
+  static bool attr[2] = {false, false};
+  auto go = [&](auto kern) {
+    if (!attr[a.prec]) {
+      DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+      attr[a.prec] = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
+                       (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
+  };
+  if (a.prec == 1)
+    go(stem_pool_kernel<1>);
+  else
+    go(stem_pool_kernel<0>);
+  set_last_conv_config(a.prec == 1 ? "stem_pool<bf16>" : "stem_pool<f16x3>");
   DD_HIP_CHECK(hipGetLastError());
   return true;
 }

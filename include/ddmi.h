@@ -161,6 +161,9 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
  * bias)) on the f16x3 kernel (synchronous; weights split on the host as dd_create does). */
 int dd_op_stem_pool_x3(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out,
                        unsigned* flags, void* stream);
+/* The same with the arithmetic chosen: prec 0 = f16x3, 1 = bf16 (one bf16 product per MAC). */
+int dd_op_stem_pool(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out, int prec,
+                    unsigned* flags, void* stream);
 /* C (M,N) = A (M,K) . W(N,K)^T [+ bias] [+ res (M,N)] [relu] */
 int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,
                int relu, void* stream);

@@ -160,6 +160,61 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
     assert int(flags.item()) == 0
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p,res,route", [
+    (64, 8, 32, 512, 512, 3, 1, 1, True, "conv_x6<8,32,128,4,2,bf16>"),     # image layer4
+    (16, 32, 128, 128, 128, 3, 1, 1, True, "conv_x6<16,16,128,4,2,bf16>"),  # layer2 3x3
+    (4, 64, 256, 64, 64, 3, 1, 1, False, "conv_x6<16,16,64,4,2,bf16>"),     # layer1 (8-wave BN 64 form)
+    (2, 12, 70, 128, 100, 3, 1, 1, True, "conv_x6<8,32,64,4,2,bf16>"),      # ragged H / W / N, 8 x 32 tiles
+    (1, 160, 128, 512, 2048, 1, 1, 0, False, "conv_x5<256,256,bf16>"),      # GPT MLP-up (M = 20480)
+    (64, 64, 256, 64, 256, 1, 1, 0, True, "conv_x5<256,256,bf16>"),         # ResNet-50 layer1 expand 1x1
+    (64, 64, 256, 64, 128, 3, 2, 1, False, "conv_x5<256,128,bf16>"),        # stage entry 3x3 / s2
+    (16, 64, 64, 36, 64, 3, 1, 1, False, "conv_x5<256,64,bf16>"),           # generic K (Cin % 32 != 0)
+    (3, 5, 7, 320, 40, 1, 1, 0, True, "conv_x3<64,64,bf16>"),               # small grid: register-staged kernel
+])
+def test_conv2d_bf16(gpu, B, H, W, Cin, Cout, k, s, p, res, route):
+    """bf16 mode (configs C2-bf16 / C4): one bf16 product per MAC on the direct 3x3 kernel (64-channel K
+    chunks), the LDS-DMA implicit GEMM (A converted at fragment-read time) or conv_x3. Reference: the same
+    conv on bf16-rounded operands in fp64 (only the fp32 accumulation order differs), 1e-4 of max|ref|;
+    and vs the unrounded conv, bf16 class."""
+    x = rnd(B, Cin, H, W, seed=71)
+    w = rnd(Cout, Cin, k, k, seed=72, scale=1.0 / np.sqrt(Cin * k * k))
+    b = rnd(Cout, seed=73)
+    ref0 = F.conv2d(x.double(), w.double(), b.double(), s, p)
+    r = rnd(*ref0.shape, seed=74) if res else None
+    # the kernels round x to bf16 (RNE) and use the bf16 image of w * 2^e (exact scaling)
+    ref_b = F.relu(F.conv2d(x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double(), b.double(), s, p)
+                   + (r.double() if res else 0))
+    ref = F.relu(ref0 + (r.double() if res else 0))
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win, bin_ = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b)
+    rin = g(r.permute(0, 2, 3, 1)) if res else None
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(),
+                           rin.data_ptr() if res else None, out.data_ptr(), Cout, k, k, s, p, 1, 1,
+                           flags.data_ptr(), None), gpu)
+    assert gpu.dd_op_last_kernel().decode() == route
+    close(out.permute(0, 3, 1, 2), ref_b, 1e-4)
+    close(out.permute(0, 3, 1, 2), ref, 3e-2)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 256), (1, 40, 72), (2, 37, 50)])
+def test_stem_pool_bf16(gpu, B, H, W):
+    """bf16 fused stem (one bf16 product per MAC) vs PyTorch fp64 on bf16-rounded operands."""
+    x = rnd(B, 4, H, W, seed=81).abs()
+    x[:, 3] = 0.0
+    w = rnd(64, 4, 7, 7, seed=82, scale=1.0 / np.sqrt(196))
+    b = rnd(64, seed=83)
+    xb, wb = x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double()
+    ref = F.max_pool2d(F.relu(F.conv2d(xb, wb, b.double(), 2, 3)), 3, 2, 1)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win, bin_ = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b)
+    ok(gpu.dd_op_stem_pool(xin.data_ptr(), B, H, W, win.data_ptr(), bin_.data_ptr(), out.data_ptr(), 1,
+                           flags.data_ptr(), None), gpu)
+    assert gpu.dd_op_last_kernel().decode() == "stem_pool<bf16>"
+    close(out.permute(0, 3, 1, 2), ref, 1e-4)
+
+
 def test_conv2d_f16x3_flags_overflow(gpu):
     """An activation beyond the fp16 range must raise DD_NUM_F16_OVERFLOW_BIT (never pass silently)."""
     x = rnd(1, 32, 8, 8, seed=15)

@@ -168,23 +168,70 @@ def test_vanilla_ddim_schedule_matches_oracle(gpu_model, seeded_sd, mode):
     assert l2 <= WAYPOINT_L2_TOL
 
 
-def test_bf16_mode_is_reduced_precision_but_sane(gpu_model, seeded_sd):
-    """DD_GEMM_BF16 (configs C2-bf16 / C4): one bf16 product per MAC. Reported, loosely bounded:
-    the reference's own bf16 autocast is 0.06-0.08 m off fp32."""
+# bf16 mode (configs C2-bf16 / C4: one bf16 product per MAC) is NOT a parity mode: a near-tie of the 20 cls
+# logits can flip the selected mode. Its bar is on the PRE-argmax tensors against the fp32 oracle: every
+# mode's 8 waypoints (last step, last layer; per-mode L2, max over scenes and modes), every cls logit and the
+# mode agreement (argmax equal) must be no worse than BOTH a fixed bar and the reference path's own bf16
+# (the oracle under torch.autocast(cpu, bfloat16) - the reference's bf16 class) on the same batch.
+BF16_ALLMODE_TOL = 0.1   # m
+BF16_CLS_TOL = 0.1       # logit
+BF16_AGREE = 0.9
+
+
+def _bf16_stats(out, ref, B):
+    reg, rreg = out["poses_reg"].float().numpy(), ref["poses_reg"].numpy()
+    return {"allmode": waypoint_l2(reg.reshape(B * 20, 8, 3), rreg.reshape(B * 20, 8, 3)),
+            "cls": float(np.abs(out["poses_cls"].float().numpy() - ref["poses_cls"].numpy()).max()),
+            "agree": float((out["poses_cls"].float().numpy().argmax(-1) == ref["poses_cls"].numpy().argmax(-1)).mean()),
+            "sel": waypoint_l2(out["trajectory"].float().numpy(), ref["trajectory"].numpy())}
+
+
+def _bf16_bar(out, om, args, B, tag):
+    ref = om.forward(*args, heads=False)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        ac = _bf16_stats(om.forward(*args, heads=False), ref, B)
+    st = _bf16_stats(out, ref, B)
+    _report([f"== {tag}: all-mode waypoint L2 {st['allmode']:.3e} m (reference bf16 autocast {ac['allmode']:.3e}), "
+             f"cls max dev {st['cls']:.3e} ({ac['cls']:.3e}), mode agreement {st['agree']:.3f} ({ac['agree']:.3f}), "
+             f"selected-trajectory L2 {st['sel']:.3e} ({ac['sel']:.3e}) [bf16: reduced precision]"])
+    assert st["allmode"] <= max(BF16_ALLMODE_TOL, ac["allmode"]), (st, ac)
+    assert st["cls"] <= max(BF16_CLS_TOL, ac["cls"]), (st, ac)
+    assert st["agree"] >= min(BF16_AGREE, ac["agree"]), (st, ac)
+
+
+def test_bf16_mode_resnet34(gpu_model, seeded_sd):
+    """C2-bf16: ResNet-34, B = 8, vs the fp32 oracle under the bf16 bar."""
     from oracle.model import OracleModel
     from diffusiondrive_amd.weights import synthetic_inputs
-    inp = synthetic_inputs(4, 1234)
-    ref = OracleModel(seeded_sd).forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"],
-                                         inp["noise"], heads=False)
+    inp = synthetic_inputs(8, 1234)
+    args = (inp["camera_feature"], inp["lidar_feature"], inp["status_feature"], inp["noise"])
     feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
     gpu_model.set_gemm_mode("bf16")
     try:
-        out = gpu_model.forward(feats, noise=torch.from_numpy(inp["noise"]))
+        out = gpu_model.forward(feats, noise=torch.from_numpy(inp["noise"]), modes=True)
     finally:
         gpu_model.set_gemm_mode("fp32")
-    l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
-    _report([f"== bf16 mode B=4: waypoint L2 vs fp32 oracle {l2:.3e} (reduced precision, not parity)"])
-    assert np.isfinite(l2) and l2 < 1.0
+    _bf16_bar(out, OracleModel(seeded_sd), args, 8, "bf16 resnet34 B=8")
+
+
+def test_bf16_resnet50_batch64_config_c4():
+    """BASELINE config C4 as stated: ResNet-50 image trunk (transfuser_backbone.py:67-93 channel adaptation),
+    bf16, B = 64, vs the fp32 CPU oracle under the bf16 bar (every conv of the trunks on the bf16 conv_x6 /
+    stem_pool / conv_x3 kernels)."""
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
+    from oracle.model import OracleModel
+    cfg = TransfuserConfig(image_architecture="resnet50")
+    sd = seeded_state_dict(cfg, 3)
+    B = 64
+    inp = synthetic_inputs(B, 1234, cfg)
+    args = (inp["camera_feature"], inp["lidar_feature"], inp["status_feature"], inp["noise"])
+    m = DiffusionDriveModel(cfg, sd, device=0, gemm="bf16")
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    out = m.forward(feats, noise=torch.from_numpy(inp["noise"]), modes=True)
+    assert m.numerics_flags() == 0
+    _bf16_bar(out, OracleModel(sd, cfg), args, B, "C4 resnet50 bf16 B=64")
 
 
 def test_gathered_value_rows_match_dense_map(gpu_model):
