@@ -62,6 +62,7 @@ _SIGS = {
                               ctypes.POINTER(ctypes.c_size_t), c_void_p]),
     "dd_op_last_error": (ctypes.c_char_p, []),
     "dd_op_last_kernel": (ctypes.c_char_p, []),
+    "dd_op_mk_linear": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p, ctypes.c_int, c_void_p]),
     "dd_build_camera": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int,
                                        ctypes.c_int, c_void_p]),
     "dd_build_lidar": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int,

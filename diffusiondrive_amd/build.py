@@ -15,15 +15,19 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 BUILD = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libddmi.so")
 ARCH = os.environ.get("DDMI_ARCH", "gfx950")
-SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "attention.hip", "stem_pool.hip", "features.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
+# DDMI_BUILD_VARIANT=stamps: a diagnostic library (libddmi_stamps.so, load it with DDMI_LIB) whose decoder
+# megakernel records per-phase clock stamps (tools/debug/mk_stamps.py); the product library has none
+VARIANT = os.environ.get("DDMI_BUILD_VARIANT", "")
+LIB = os.path.join(HERE, "libddmi.so" if not VARIANT else f"libddmi_{VARIANT}.so")
+VARIANT_FLAGS = {"": [], "stamps": ["-DDDMI_MK_STAMPS"]}[VARIANT]
+SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "decoder_mk.hip", "attention.hip", "stem_pool.hip", "features.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         "-I", CSRC, "-I", INCLUDE]
+         "-I", CSRC, "-I", INCLUDE] + VARIANT_FLAGS
 # Elementwise / decoder arithmetic must round like PyTorch-CPU's separate mul and add kernels
 # (no a*b+c -> fma contraction): the DDIM / norm_odo / bilinear-weight chains feed the BEV
 # sampling positions, which are sensitive at the 1e-5 m level.
-PER_SOURCE_FLAGS = {"decoder.hip": ["-ffp-contract=off"], "elementwise.hip": ["-ffp-contract=off"],
+PER_SOURCE_FLAGS = {"decoder.hip": ["-ffp-contract=off"], "decoder_mk.hip": ["-ffp-contract=off"], "elementwise.hip": ["-ffp-contract=off"],
                     "runtime.cpp": ["-ffp-contract=off"]}
 
 
@@ -66,7 +70,7 @@ def build(verbose: bool = True) -> str:
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(lambda s: _compile(hipcc, s, hdr), SOURCES))
     key = hashlib.sha256("".join(objs).encode()).hexdigest()[:16]
-    stamp = os.path.join(BUILD, "lib.stamp")
+    stamp = os.path.join(BUILD, f"lib{VARIANT}.stamp")
     if os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read() == key:
         return LIB
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]

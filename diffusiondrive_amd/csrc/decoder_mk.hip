@@ -1,0 +1,813 @@
+// Decoder-layer megakernel: one launch per (denoise step, decoder layer) for the whole batch, one
+// 512-thread workgroup per scene (TrajectoryHead.forward_test, transfuser_model_v2.py:578-641, with
+// CustomTransformerDecoderLayer :297-382 inside). The per-layer chain of the unfused path - about 20
+// launches of 5-25 us (12 M = 1280 GEMMs, 5 LayerNorms, BEV sampling, agent MHA, finalize, DDIM) -
+// becomes one launch whose phases are separated by workgroup barriers only: every row of the chain
+// is a trajectory query of ONE scene, so no phase needs another workgroup's data.
+//
+// Per scene (20 queries; MFMA row tile 32, rows 20..31 zero):
+//   [layer 0] points = denorm(clamp(x_t)); gen_sineembed_for_position (blocks.py:22-40) -> 512 / query;
+//             plan_anchor_encoder Linear 512 -> 256, ReLU, LN, Linear 256 -> 256 (:459-462) = traj_feature
+//   BEV attention (blocks.py:88-129): logits = Linear 256 -> 8 (fp32 VALU), softmax, 4-tap bilinear
+//             gather of the gathered value_proj rows (slots), output_proj + residual
+//   agent cross-attention: q projection, 8-head attention over the scene's 30 agent K / V (staged in
+//             LDS), out_proj + residual, norm1; ego attention (hoisted: + ego row), norm2
+//   FFN 256 -> 1024 -> 256 (four 256-wide hidden chunks, the second GEMM accumulating in registers),
+//             norm3, FiLM (ModulationLayer, :259-294)
+//   heads (:208-256): cls [Linear, ReLU, LN] x 2 -> Linear 256 -> 1; reg Linear-ReLU-Linear-ReLU ->
+//             Linear 256 -> 24; reg[..., :2] += points, heading = tanh * pi (:376-380)
+//   [layer 0] the BEV taps of layer 1 (its points = this layer's reg xy) deduplicated for the gathered
+//             value_proj conv that runs between the two launches
+//   [layer 1] DDIM step (eta 0, prediction 'sample', clip; diffusers semantics) and the taps of the next
+//             step's layer 0; or, at the last step, the argmax mode selection (:637-641)
+//
+// Arithmetic: the 256-wide Linears are f16x3 on v_mfma_f32_32x32x16_f16 exactly as conv_x3 (weights
+// pre-split with the same per-column power-of-two scale, stored in MFMA-fragment order so a wave's
+// B fragment is one contiguous 2 KB read; activations split once when their producer writes them to
+// LDS); the 8 / 1 / 24-wide heads, softmaxes, LayerNorms, attention, geometry and DDIM in fp32 VALU.
+// Compiled with -ffp-contract=off like decoder.hip: the geometry / DDIM chains round like PyTorch.
+//
+// LDS (141 KB, one workgroup per CU): two fp32 [32][260] row buffers, two split [32][264] hi / lo
+// A-operand buffers (together the K = 512 embedding operand, or the scene's agent K / V during the
+// attention), small per-query state. Weights stream from L2 straight into the MFMA operand registers.
+#include "decoder_mk.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace ddmi {
+
+namespace {
+
+typedef _Float16 mk_h8 __attribute__((ext_vector_type(8)));
+typedef float mk_f16 __attribute__((ext_vector_type(16)));
+
+constexpr int kQ = 20, kP = 8, kD = 256, kA = 30, kNH = 8, kHD = 32, kHV = 64, kFF = 1024;
+constexpr int kQP = kQ * kP;
+constexpr int NT = 512;
+constexpr int FP = 260;   // fp32 row pitch (floats)
+constexpr int HP = 264;   // split row pitch (halfs), K = 256: 528 B, 16 mod 256 -> conflict-free b128 reads
+constexpr int HP2 = 520;  // split row pitch (halfs), K = 512: 1040 B
+constexpr int OFF_T1 = 32 * FP * 4;
+constexpr int OFF_SA = 2 * 32 * FP * 4;               // 66560
+constexpr int SPLIT_BYTES = 32 * HP * 2;              // one hi or lo image, K = 256
+constexpr int OFF_SB = OFF_SA + 2 * SPLIT_BYTES;      // 100352
+constexpr int OFF_SMALL = OFF_SB + 2 * SPLIT_BYTES;   // 134144
+// small per-query state (floats)
+constexpr int S_W8 = 0;                 // [20][8] BEV point weights
+constexpr int S_PTS = S_W8 + kQP;       // [160][2] points of this layer
+constexpr int S_PN = S_PTS + 2 * kQP;   // [160][2] next points
+constexpr int S_RR = S_PN + 2 * kQP;    // [20][24] reg head raw
+constexpr int S_REG = S_RR + kQ * 24;   // [160][3] reg output
+constexpr int S_CLS = S_REG + 3 * kQP;  // [20] cls logits
+constexpr int S_END = S_CLS + 32;
+constexpr int LDS_BYTES = OFF_SMALL + S_END * 4;
+static_assert(2 * 32 * HP2 * 2 <= 4 * SPLIT_BYTES, "K = 512 operand fits the two split buffers");
+static_assert(kA * 2 * kD * 4 <= 4 * SPLIT_BYTES, "agent K / V fit the two split buffers");
+static_assert(4096 * 4 + NT * 4 <= 32 * FP * 4, "dedup table fits a row buffer");
+static_assert(kNH * kQ * 33 <= 32 * FP, "attention probabilities fit a row buffer");
+
+__device__ inline float norm_x(float x) { return 2.f * (x + 1.2f) / 56.9f - 1.f; }
+__device__ inline float norm_y(float y) { return 2.f * (y + 20.f) / 46.f - 1.f; }
+__device__ inline float denorm_x(float x) { return (x + 1.f) / 2.f * 56.9f - 1.2f; }
+__device__ inline float denorm_y(float y) { return (y + 1.f) / 2.f * 46.f - 20.f; }
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// F.grid_sample bilinear geometry (align_corners=False) of a trajectory point (blocks.py:101-122),
+// the arithmetic of decoder.hip's bev_tap_geometry
+__device__ inline void tap_geom(float tx, float ty, int& x0, int& y0, float wt[4]) {
+  const float gx = ty * (1.0f / 32.0f);  // grid x (width) <- trajectory y
+  const float gy = tx * (1.0f / 32.0f);  // grid y (height) <- trajectory x
+  const float ix = ((gx + 1.f) * (float)kHV - 1.f) / 2.f;
+  const float iy = ((gy + 1.f) * (float)kHV - 1.f) / 2.f;
+  const float fx = floorf(ix), fy = floorf(iy);
+  x0 = (int)fx;
+  y0 = (int)fy;
+  const int x1 = x0 + 1, y1 = y0 + 1;
+  wt[0] = ((float)x1 - ix) * ((float)y1 - iy);
+  wt[1] = (ix - (float)x0) * ((float)y1 - iy);
+  wt[2] = ((float)x1 - ix) * (iy - (float)y0);
+  wt[3] = (ix - (float)x0) * (iy - (float)y0);
+}
+
+// the scene's distinct tap pixels (pixel order) -> rows[b*cap ..], -1 past the count; each tap's
+// compact row -> slots (bev_tap_dedup_kernel's algorithm with the workgroup's threads)
+__device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int* rows, int* slots) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  constexpr int HW = kHV * kHV, cap = kQP * 4;
+  const int64_t base = (int64_t)b * cap;
+  for (int e = tid; e < HW; e += nt) table[e] = 0;
+  __syncthreads();
+  for (int u = tid; u < kQP; u += nt) {
+    int x0, y0;
+    float wt[4];
+    tap_geom(pts[2 * u], pts[2 * u + 1], x0, y0, wt);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int yy = y0 + (t >> 1), xx = x0 + (t & 1);
+      if ((unsigned)yy < (unsigned)kHV && (unsigned)xx < (unsigned)kHV) table[yy * kHV + xx] = 1;
+    }
+  }
+  __syncthreads();
+  const int E = (HW + nt - 1) / nt;
+  int cnt = 0;
+  for (int e = tid * E; e < min(HW, tid * E + E); ++e) cnt += table[e];
+  scan[tid] = cnt;
+  __syncthreads();
+  for (int off = 1; off < nt; off <<= 1) {
+    const int v = tid >= off ? scan[tid - off] : 0;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  int r = scan[tid] - cnt;
+  const int total = scan[nt - 1];
+  for (int e = tid * E; e < min(HW, tid * E + E); ++e)
+    if (table[e]) {
+      table[e] = r;
+      rows[base + r] = b * HW + e;
+      ++r;
+    }
+  for (int j = total + tid; j < cap; j += nt) rows[base + j] = -1;
+  __syncthreads();
+  for (int u = tid; u < kQP; u += nt) {
+    int x0, y0;
+    float wt[4];
+    tap_geom(pts[2 * u], pts[2 * u + 1], x0, y0, wt);
+    int4 sl;
+    auto slot = [&](int yy, int xx) {
+      return ((unsigned)yy < (unsigned)kHV && (unsigned)xx < (unsigned)kHV) ? (int)(base + table[yy * kHV + xx]) : -1;
+    };
+    sl.x = slot(y0, x0);
+    sl.y = slot(y0, x0 + 1);
+    sl.z = slot(y0 + 1, x0);
+    sl.w = slot(y0 + 1, x0 + 1);
+    *reinterpret_cast<int4*>(slots + ((int64_t)b * kQP + u) * 4) = sl;
+  }
+}
+
+// acc += A[32][aks*16 .. (aks+NKS)*16) (split LDS images, row pitch hp halfs) x W[:, wks*16 ..]^T for
+// the 32 output columns of tile nt: the NKS fragment pairs of the wave are loaded first (2 KB contiguous
+// per fragment per wave), then 3 f16 MFMAs per k16 step (small terms first, as conv_x3)
+template <int NKS>
+__device__ inline void mk_gemm(const char* ahi, const char* alo, int hp, const MkLin& L, int nt, int wks,
+                               mk_f16& acc, int aks = 0) {
+  // a ring of PF fragment pairs in flight (PF x 32 B per lane); fence the scheduler at both ends so the
+  // next GEMM's loads are not hoisted into this one (their registers would not fit beside these)
+  constexpr int PF = 8;
+  static_assert(NKS % PF == 0, "ring");
+  __builtin_amdgcn_sched_barrier(0);
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  const uint4* wb = L.w + ((size_t)(nt * L.nks + wks) * 64 + lane) * 2;
+  uint4 bh[PF], bl[PF];
+#pragma unroll
+  for (int s = 0; s < PF; ++s) {
+    bh[s] = wb[s * 128];
+    bl[s] = wb[s * 128 + 1];
+  }
+  const int aoff = li * hp * 2 + hh * 16 + aks * 32;
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const mk_h8 ah = *reinterpret_cast<const mk_h8*>(ahi + aoff + s * 32);
+    const mk_h8 al = *reinterpret_cast<const mk_h8*>(alo + aoff + s * 32);
+    const mk_h8 wh = __builtin_bit_cast(mk_h8, bh[s % PF]), wl = __builtin_bit_cast(mk_h8, bl[s % PF]);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wh, acc, 0, 0, 0);
+    if (s + PF < NKS) {
+      bh[s % PF] = wb[(s + PF) * 128];
+      bl[s % PF] = wb[(s + PF) * 128 + 1];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ inline void zero_acc(mk_f16& acc) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+}
+
+// epilogue: f(row, col, acc * s + b) for this lane's 16 accumulator rows (C/D map of the 32x32 MFMA:
+// column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)); non-finite accumulators of live rows
+// (an activation beyond the fp16 range met the split) raise the numerics flag
+template <class F>
+__device__ inline void mk_epi(const mk_f16& acc, const MkLin& L, int nt, unsigned* flags, F&& f) {
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  const int col = nt * 32 + li;
+  const float s = L.s[col], bias = L.b ? L.b[col] : 0.f;
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
+    if (row < kQ) bad |= !__builtin_isfinite(acc[r]);
+    f(row, col, acc[r] * s + bias);
+  }
+  if (bad && flags) atomicOr(flags, (unsigned)DD_NUM_F16_OVERFLOW);
+}
+
+__device__ inline void st_split(char* hi, int hp, int row, int col, float v) {
+  const _Float16 h = (_Float16)v;
+  const _Float16 l = (_Float16)(v - (float)h);
+  reinterpret_cast<_Float16*>(hi)[row * hp + col] = h;
+  reinterpret_cast<_Float16*>(hi + 32 * hp * 2)[row * hp + col] = l;
+}
+
+// 4 consecutive columns of a row into a split buffer (8 B hi, 8 B lo)
+__device__ inline void st_split4(char* hi, int hp, int row, int c4, float4 v) {
+  _Float16 h[4], l[4];
+  const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = (_Float16)x[e];
+    l[e] = (_Float16)(x[e] - (float)h[e]);
+  }
+  uint2 hv, lv;
+  __builtin_memcpy(&hv, h, 8);
+  __builtin_memcpy(&lv, l, 8);
+  *reinterpret_cast<uint2*>(hi + (row * hp + c4) * 2) = hv;
+  *reinterpret_cast<uint2*>(hi + 32 * hp * 2 + (row * hp + c4) * 2) = lv;
+}
+
+// LayerNorm(256) of one row held as one float4 per lane (layernorm_v4's arithmetic, eps 1e-5)
+__device__ inline float4 ln256(float4 v, const float* g, const float* b, int lane) {
+  float s = (v.x + v.y) + (v.z + v.w);
+  s = wave_sum(s);
+  const float mean = s / 256.f;
+  const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+  float q = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+  q = wave_sum(q);
+  const float rstd = rsqrtf(q / 256.f + 1e-5f);
+  const float4 gg = reinterpret_cast<const float4*>(g)[lane], bb = reinterpret_cast<const float4*>(b)[lane];
+  float4 o;
+  o.x = (v.x - mean) * rstd * gg.x + bb.x;
+  o.y = (v.y - mean) * rstd * gg.y + bb.y;
+  o.z = (v.z - mean) * rstd * gg.z + bb.z;
+  o.w = (v.w - mean) * rstd * gg.w + bb.w;
+  return o;
+}
+
+__device__ inline float4 relu4(float4 v) {
+  return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+}
+
+__global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* X1 = reinterpret_cast<float*>(lds);
+  float* T1 = reinterpret_cast<float*>(lds + OFF_T1);
+  char* SA = lds + OFF_SA;  // hi image; lo image at + SPLIT_BYTES
+  char* SB = lds + OFF_SB;
+  float* SM = reinterpret_cast<float*>(lds + OFF_SMALL);
+  const float* __restrict__ dim_t = a.dim_t;
+  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int row0 = b * kQ;  // first global query row of the scene
+  const MkLayer& L = a.L;
+  // diagnostic phase stamps (a separate build, DDMI_BUILD_VARIANT=stamps: -DDDMI_MK_STAMPS, and
+  // MkArgs::stamps set by DDMI_MK_STAMPS=1): shader clock after each phase barrier. Compiled out of the
+  // product library (the stamp stores cost registers).
+#ifdef DDMI_MK_STAMPS
+  __shared__ unsigned long long st_lds[40];
+  if (tid < 40) st_lds[tid] = 0ull;
+  auto stamp = [&](int k) {
+    if (tid == 0) st_lds[k] = __builtin_amdgcn_s_memtime();
+  };
+#else
+  auto stamp = [](int) {};
+#endif
+  stamp(0);
+
+  // ================================================================ layer 0: points, embedding, anchor encoder
+  if (a.layer == 0) {
+    for (int t = tid; t < kQP; t += NT) {
+      const float* im = a.imgx + ((int64_t)b * kQP + t) * 2;
+      const float cx = fminf(fmaxf(im[0], -1.f), 1.f);
+      const float cy = fminf(fmaxf(im[1], -1.f), 1.f);
+      const float px = denorm_x(cx), py = denorm_y(cy);
+      SM[S_PTS + 2 * t] = px;
+      SM[S_PTS + 2 * t + 1] = py;
+      a.pts[((int64_t)b * kQP + t) * 2] = px;
+      a.pts[((int64_t)b * kQP + t) * 2 + 1] = py;
+    }
+    __syncthreads();
+    stamp(1);
+    // gen_sineembed_for_position: query q, point p, slot d -> column p * 64 + d of the K = 512 operand;
+    // slots 2f and 2f + 1 share the angle (sin / cos); the padding queries' rows are zero
+    char* EH = SA;  // [32][HP2] hi, then [32][HP2] lo
+    for (int e = tid; e < kQ * kP * 32; e += NT) {
+      const int t = e >> 5, f = e & 31;  // t = q * P + p; f = coordinate half (y: 0..15, x: 16..31) x frequency
+      const int q = t >> 3, p = t & 7;
+      const float u = ((f < 16) ? SM[S_PTS + 2 * t + 1] : SM[S_PTS + 2 * t]) * 6.283185307179586f;
+      const float ang = u / dim_t[f & 15];
+      const int col = p * 64 + 2 * f;
+      st_split(EH, HP2, q, col, sinf(ang));
+      st_split(EH, HP2, q, col + 1, cosf(ang));
+    }
+    for (int e = tid; e < (32 - kQ) * 512; e += NT) st_split(EH, HP2, kQ + (e >> 9), e & 511, 0.f);
+    __syncthreads();
+    mk_f16 acc;
+    zero_acc(acc);
+    mk_gemm<16>(EH, EH + 32 * HP2 * 2, HP2, a.A.pa0, wave, 0, acc);
+    mk_gemm<16>(EH, EH + 32 * HP2 * 2, HP2, a.A.pa0, wave, 16, acc, 16);
+    mk_epi(acc, a.A.pa0, wave, a.flags, [&](int row, int col, float v) { T1[row * FP + col] = fmaxf(v, 0.f); });
+    __syncthreads();
+    stamp(2);
+    for (int q = wave; q < 32; q += 8) {
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < kQ) o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], a.A.pa2g, a.A.pa2b, lane);
+      st_split4(SA, HP, q, lane * 4, o);
+    }
+    __syncthreads();
+    stamp(3);
+    zero_acc(acc);
+    mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, a.A.pa3, wave, 0, acc);
+    mk_epi(acc, a.A.pa3, wave, a.flags, [&](int row, int col, float v) {
+      if (row < kQ) {
+        X1[row * FP + col] = v;
+        a.tfe[(int64_t)(row0 + row) * kD + col] = v;
+      }
+    });
+  } else {
+    for (int e = tid; e < kQ * 64; e += NT) {
+      const int q = e >> 6, c4 = (e & 63) * 4;
+      *reinterpret_cast<float4*>(X1 + q * FP + c4) =
+          *reinterpret_cast<const float4*>(a.tfe + (int64_t)(row0 + q) * kD + c4);
+    }
+    for (int t = tid; t < kQP; t += NT) {
+      SM[S_PTS + 2 * t] = a.pts[((int64_t)b * kQP + t) * 2];
+      SM[S_PTS + 2 * t + 1] = a.pts[((int64_t)b * kQP + t) * 2 + 1];
+    }
+  }
+  __syncthreads();
+  stamp(4);
+
+  // ================================================================ GridSampleCrossBEVAttention
+  // logits = attention_weights(query) (Linear 256 -> 8, fp32), softmax over the 8 points: a wave per
+  // query, a float4 of channels per lane (the 8 weight rows held in registers), wave reductions
+  {
+    float4 wr[kP];
+#pragma unroll
+    for (int p = 0; p < kP; ++p) wr[p] = reinterpret_cast<const float4*>(L.attw_w + p * kD)[lane];
+    for (int q = wave; q < kQ; q += 8) {
+      const float4 x = reinterpret_cast<const float4*>(X1 + q * FP)[lane];
+      float lg[kP];
+#pragma unroll
+      for (int p = 0; p < kP; ++p)
+        lg[p] = wave_sum((x.x * wr[p].x + x.y * wr[p].y) + (x.z * wr[p].z + x.w * wr[p].w)) + L.attw_b[p];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int p = 0; p < kP; ++p) mx = fmaxf(mx, lg[p]);
+      float s = 0.f;
+#pragma unroll
+      for (int p = 0; p < kP; ++p) {
+        lg[p] = expf(lg[p] - mx);
+        s += lg[p];
+      }
+      const float inv = 1.f / s;
+      if (lane < kP) {
+        float v = 0.f;
+#pragma unroll
+        for (int p = 0; p < kP; ++p) v = lane == p ? lg[p] * inv : v;
+        SM[S_W8 + q * kP + lane] = v;
+      }
+    }
+  }
+  __syncthreads();
+  stamp(5);
+  // sum_p w_p * bilinear(value, point p): one wave per query, a float4 of channels per lane; the value
+  // rows are the gathered value_proj rows of the scene's distinct tap pixels (slots)
+  for (int q = wave; q < 32; q += 8) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < kQ) {
+#pragma unroll
+      for (int g = 0; g < kP; g += 2) {
+        float4 v[2][4];
+        float wt[2][4];
+        bool ok[2][4];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const int t = q * kP + g + pp;
+          int x0, y0;
+          tap_geom(SM[S_PTS + 2 * t], SM[S_PTS + 2 * t + 1], x0, y0, wt[pp]);
+          const int4 sl = *reinterpret_cast<const int4*>(a.slots + ((int64_t)b * kQP + t) * 4);
+          const int sv[4] = {sl.x, sl.y, sl.z, sl.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            ok[pp][u] = sv[u] >= 0;  // slot -1 <=> the tap reads zero padding
+            v[pp][u] = ok[pp][u] ? *reinterpret_cast<const float4*>(a.vrows + (int64_t)sv[u] * kD + lane * 4)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          float4 sp = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (ok[pp][u]) {
+              sp.x += v[pp][u].x * wt[pp][u];
+              sp.y += v[pp][u].y * wt[pp][u];
+              sp.z += v[pp][u].z * wt[pp][u];
+              sp.w += v[pp][u].w * wt[pp][u];
+            }
+          }
+          const float wp = SM[S_W8 + q * kP + g + pp];
+          acc.x += wp * sp.x;
+          acc.y += wp * sp.y;
+          acc.z += wp * sp.z;
+          acc.w += wp * sp.w;
+        }
+      }
+      *reinterpret_cast<float4*>(a.gs_out + (int64_t)(row0 + q) * kD + lane * 4) = acc;
+    }
+    st_split4(SA, HP, q, lane * 4, acc);
+  }
+  __syncthreads();
+  stamp(6);
+  // output_proj + residual (blocks.py:127-129): x1 = W gso + b + query
+  mk_f16 acc;
+  zero_acc(acc);
+  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.outp, wave, 0, acc);
+  mk_epi(acc, L.outp, wave, a.flags, [&](int row, int col, float v) {
+    float x = 0.f;
+    if (row < kQ) {
+      x = v + X1[row * FP + col];
+      X1[row * FP + col] = x;
+    }
+    st_split(SB, HP, row, col, x);
+  });
+  __syncthreads();
+  stamp(7);
+
+  // ================================================================ cross_agent_attention (+ norm1)
+  zero_acc(acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ag_q, wave, 0, acc);
+  mk_epi(acc, L.ag_q, wave, a.flags, [&](int row, int col, float v) {
+    if (row < kQ) T1[row * FP + col] = v;
+  });
+  // the scene's agent K | V rows into the two split buffers (free until the output is written; the
+  // barrier retires every wave's q-projection reads of SB first)
+  __syncthreads();
+  stamp(8);
+  float* KV = reinterpret_cast<float*>(SA);
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.akv + (int64_t)b * kA * 2 * kD);
+    for (int e = tid; e < kA * 2 * kD / 4; e += NT) reinterpret_cast<float4*>(KV)[e] = src[e];
+  }
+  __syncthreads();
+  stamp(9);
+  {
+    // wave = head h, lane = (query i = lane & 31, half = lane >> 5): scores of keys half*15 .. +14
+    const int h = wave, i = lane & 31, half = lane >> 5;
+    const bool live = i < kQ;
+    float qv[kHD];
+#pragma unroll
+    for (int e = 0; e < kHD; e += 4) {
+      const float4 v = live ? *reinterpret_cast<const float4*>(T1 + i * FP + h * kHD + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      qv[e] = v.x;
+      qv[e + 1] = v.y;
+      qv[e + 2] = v.z;
+      qv[e + 3] = v.w;
+    }
+    __syncthreads();  // every lane holds its query slice: T1 becomes the probability buffer
+    stamp(10);
+    const float scale = 1.0f / sqrtf((float)kHD);
+    constexpr int KH = kA / 2;
+    float sc[KH];
+    float m = -INFINITY;
+#pragma unroll
+    for (int jj = 0; jj < KH; ++jj) {
+      const int j = half * KH + jj;
+      const float* kr = KV + j * 2 * kD + h * kHD;
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < kHD; ++e) d += qv[e] * kr[e];
+      sc[jj] = d * scale;
+      m = fmaxf(m, sc[jj]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < KH; ++jj) {
+      sc[jj] = expf(sc[jj] - m);
+      sum += sc[jj];
+    }
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+    // [head][query][key] probabilities of the live queries, pitch 33 (conflict-free column walk); the dead
+    // lanes (padding queries) read a live row and their outputs are written as zeros
+    float* pr = T1 + (h * kQ + (live ? i : kQ - 1)) * 33;
+    if (live) {
+#pragma unroll
+      for (int jj = 0; jj < KH; ++jj) pr[half * KH + jj] = sc[jj] * inv;
+    }
+    __syncthreads();
+    stamp(11);
+    float o[16];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) o[d] = 0.f;
+    for (int j = 0; j < kA; ++j) {
+      const float pj = pr[j];
+      const float* vr = KV + j * 2 * kD + kD + h * kHD + half * 16;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) o[d] += pj * vr[d];
+    }
+    __syncthreads();  // every lane is done with K / V: the split buffer takes the attention output
+    stamp(12);
+#pragma unroll
+    for (int d = 0; d < 16; d += 4)
+      st_split4(SA, HP, i, h * kHD + half * 16 + d,
+                live ? make_float4(o[d], o[d + 1], o[d + 2], o[d + 3]) : make_float4(0.f, 0.f, 0.f, 0.f));
+  }
+  __syncthreads();
+  stamp(13);
+  // out_proj + residual
+  zero_acc(acc);
+  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ag_out, wave, 0, acc);
+  mk_epi(acc, L.ag_out, wave, a.flags, [&](int row, int col, float v) {
+    if (row < kQ) X1[row * FP + col] = v + X1[row * FP + col];
+  });
+  __syncthreads();
+  stamp(14);
+  // norm1; cross_ego_attention over one key = the hoisted ego row, residual; norm2 -> FFN operand
+  for (int q = wave; q < 32; q += 8) {
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < kQ) {
+      float4 v = ln256(reinterpret_cast<const float4*>(X1 + q * FP)[lane], L.n1g, L.n1b, lane);
+      const float4 eg = reinterpret_cast<const float4*>(a.ego + (int64_t)b * kD)[lane];
+      v.x += eg.x;
+      v.y += eg.y;
+      v.z += eg.z;
+      v.w += eg.w;
+      o = ln256(v, L.n2g, L.n2b, lane);
+    }
+    st_split4(SB, HP, q, lane * 4, o);
+  }
+  __syncthreads();
+  stamp(15);
+
+  // ================================================================ FFN 256 -> 1024 -> 256, norm3, FiLM
+  mk_f16 acc2;
+  zero_acc(acc2);
+  for (int c = 0; c < kFF / kD; ++c) {
+    zero_acc(acc);
+    mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ffn0, c * 8 + wave, 0, acc);
+    mk_epi(acc, L.ffn0, c * 8 + wave, a.flags,
+           [&](int row, int col, float v) { st_split(SA, HP, row, col - c * kD, row < kQ ? fmaxf(v, 0.f) : 0.f); });
+    __syncthreads();
+    stamp(16 + 2 * c);
+    mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ffn2, wave, c * 16, acc2);
+    __syncthreads();
+    stamp(17 + 2 * c);
+  }
+  mk_epi(acc2, L.ffn2, wave, a.flags, [&](int row, int col, float v) {
+    if (row < kQ) T1[row * FP + col] = v;
+  });
+  __syncthreads();
+  stamp(24);
+  for (int q = wave; q < 32; q += 8) {
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < kQ) {
+      o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.n3g, L.n3b, lane);
+      const float4 fs = reinterpret_cast<const float4*>(a.film)[lane];
+      const float4 fb = reinterpret_cast<const float4*>(a.film + kD)[lane];
+      o.x = o.x * (1.f + fs.x) + fb.x;
+      o.y = o.y * (1.f + fs.y) + fb.y;
+      o.z = o.z * (1.f + fs.z) + fb.z;
+      o.w = o.w * (1.f + fs.w) + fb.w;
+    }
+    st_split4(SB, HP, q, lane * 4, o);
+  }
+  __syncthreads();
+  stamp(25);
+
+  // ================================================================ task decoder: cls and reg branches
+  zero_acc(acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c0, wave, 0, acc);
+  mk_epi(acc, L.c0, wave, a.flags, [&](int row, int col, float v) {
+    if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
+  });
+  zero_acc(acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.r0, wave, 0, acc);
+  mk_epi(acc, L.r0, wave, a.flags, [&](int row, int col, float v) { st_split(SA, HP, row, col, row < kQ ? fmaxf(v, 0.f) : 0.f); });
+  __syncthreads();
+  stamp(26);
+  for (int q = wave; q < 32; q += 8) {
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < kQ) o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c2g, L.c2b, lane);
+    st_split4(SB, HP, q, lane * 4, o);
+  }
+  __syncthreads();
+  stamp(27);
+  zero_acc(acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c3, wave, 0, acc);
+  mk_epi(acc, L.c3, wave, a.flags, [&](int row, int col, float v) {
+    if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
+  });
+  zero_acc(acc);
+  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.r2, wave, 0, acc);
+  mk_epi(acc, L.r2, wave, a.flags, [&](int row, int col, float v) {
+    if (row < kQ) X1[row * FP + col] = fmaxf(v, 0.f);
+  });
+  __syncthreads();
+  stamp(28);
+  // cls: LN, Linear 256 -> 1 (a wave per query); reg: Linear 256 -> 24 (a thread per output)
+  for (int q = wave; q < kQ; q += 8) {
+    const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c5g, L.c5b, lane);
+    const float4 w = reinterpret_cast<const float4*>(L.c6_w)[lane];
+    const float s = wave_sum((o.x * w.x + o.y * w.y) + (o.z * w.z + o.w * w.w));
+    if (lane == 0) {
+      const float c = s + L.c6_b[0];
+      SM[S_CLS + q] = c;
+      a.cls_out[row0 + q] = c;
+    }
+  }
+  for (int h = 0; h < 2; ++h) {
+    constexpr int NO = kP * 3 / 2;
+    float4 wr[NO];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) wr[o] = reinterpret_cast<const float4*>(L.r4_w + (h * NO + o) * kD)[lane];
+    for (int q = wave; q < kQ; q += 8) {
+      const float4 x = reinterpret_cast<const float4*>(X1 + q * FP)[lane];
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+        const float s = wave_sum((x.x * wr[o].x + x.y * wr[o].y) + (x.z * wr[o].z + x.w * wr[o].w));
+        if (lane == 0) SM[S_RR + q * kP * 3 + h * NO + o] = s + L.r4_b[h * NO + o];
+      }
+    }
+  }
+  __syncthreads();
+  stamp(29);
+  // reg[..., :2] += points; reg[..., 2] = tanh * pi (transfuser_model_v2.py:376-380)
+  for (int t = tid; t < kQP; t += NT) {
+    const float* rr = SM + S_RR + t * 3;
+    const float x = rr[0] + SM[S_PTS + 2 * t];
+    const float y = rr[1] + SM[S_PTS + 2 * t + 1];
+    const float hd = tanhf(rr[2]) * 3.14159265358979323846f;
+    float* ro = a.reg_out + ((int64_t)b * kQP + t) * 3;
+    ro[0] = x;
+    ro[1] = y;
+    ro[2] = hd;
+    SM[S_REG + 3 * t] = x;
+    SM[S_REG + 3 * t + 1] = y;
+    SM[S_REG + 3 * t + 2] = hd;
+    SM[S_PN + 2 * t] = x;
+    SM[S_PN + 2 * t + 1] = y;
+    if (a.pts_next) {
+      a.pts_next[((int64_t)b * kQP + t) * 2] = x;
+      a.pts_next[((int64_t)b * kQP + t) * 2 + 1] = y;
+    }
+  }
+  __syncthreads();
+  stamp(30);
+
+  // ================================================================ DDIM step / mode selection / next taps
+  if (a.layer == 1 && a.ddim) {
+    for (int t = tid; t < kQP; t += NT) {
+      float* im = a.imgx + ((int64_t)b * kQP + t) * 2;
+      const float x0x = norm_x(SM[S_REG + 3 * t]);
+      const float x0y = norm_y(SM[S_REG + 3 * t + 1]);
+      const float ex = (im[0] - a.sa_t * x0x) / a.sb_t;
+      const float ey = (im[1] - a.sa_t * x0y) / a.sb_t;
+      const float cx = fminf(fmaxf(x0x, -1.f), 1.f);
+      const float cy = fminf(fmaxf(x0y, -1.f), 1.f);
+      const float nx = a.sa_p * cx + a.sdir * ex;
+      const float ny = a.sa_p * cy + a.sdir * ey;
+      im[0] = nx;
+      im[1] = ny;
+      // the next step's points (traj_embed arithmetic)
+      SM[S_PN + 2 * t] = denorm_x(fminf(fmaxf(nx, -1.f), 1.f));
+      SM[S_PN + 2 * t + 1] = denorm_y(fminf(fmaxf(ny, -1.f), 1.f));
+    }
+    __syncthreads();
+    stamp(31);
+  }
+  if (a.traj && tid == 0) {
+    int best = 0;
+    float bv = SM[S_CLS];
+    for (int q = 1; q < kQ; ++q) {
+      const float v = SM[S_CLS + q];
+      if (v > bv || (v != v && bv == bv)) {  // first maximal index; NaN propagates like torch.argmax
+        bv = v;
+        best = q;
+      }
+    }
+    if (a.mode_idx) a.mode_idx[b] = best;
+    for (int e = 0; e < kP * 3; ++e) a.traj[(int64_t)b * kP * 3 + e] = SM[S_REG + best * kP * 3 + e];
+  }
+  if (a.next_rows) {
+    int* table = reinterpret_cast<int*>(T1);
+    dedup_scene(SM + S_PN, table, table + 4096, b, a.next_rows, a.next_slots);
+  }
+#ifdef DDMI_MK_STAMPS
+  stamp(32);
+  if (a.stamps && tid < 40) a.stamps[(int64_t)b * 40 + tid] = st_lds[tid];
+#endif
+}
+
+// DDIM add_noise at the truncation step (:591-597), the first step's points and their tap dedup
+__global__ __launch_bounds__(256) void decoder_mk_init_kernel(MkInitArgs a) {
+  __shared__ float pts[2 * kQP];
+  __shared__ int table[4096 + 256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  for (int t = tid; t < kQP; t += 256) {
+    const int64_t i = (int64_t)b * kQP + t;
+    const float ax = a.anchor[t * 2], ay = a.anchor[t * 2 + 1];
+    const float ix = a.sa * norm_x(ax) + a.s1a * a.noise[i * 2];
+    const float iy = a.sa * norm_y(ay) + a.s1a * a.noise[i * 2 + 1];
+    a.imgx[i * 2] = ix;
+    a.imgx[i * 2 + 1] = iy;
+    pts[2 * t] = denorm_x(fminf(fmaxf(ix, -1.f), 1.f));
+    pts[2 * t + 1] = denorm_y(fminf(fmaxf(iy, -1.f), 1.f));
+  }
+  __syncthreads();
+  dedup_scene(pts, table, table + 4096, b, a.rows, a.slots);
+}
+
+// GEMM-core test: A [32][K] fp32 -> split LDS image -> mk_gemm over 256-column units -> out
+__global__ __launch_bounds__(NT, 1) void mk_linear_test_kernel(const float* __restrict__ A, int K, MkLin W, int N,
+                                                               float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int hp = K + 8;
+  for (int e = tid; e < 32 * K; e += NT) st_split(lds, hp, e / K, e % K, A[e]);
+  __syncthreads();
+  for (int nt = wave; nt < N / 32; nt += 8) {
+    mk_f16 acc;
+    zero_acc(acc);
+    for (int ks = 0; ks < K / 16; ks += 16) mk_gemm<16>(lds, lds + 32 * hp * 2, hp, W, nt, ks, acc, ks);
+    mk_epi(acc, W, nt, nullptr, [&](int row, int col, float v) { out[row * N + col] = v; });
+  }
+}
+
+}  // namespace
+
+void pack_mk_weights(const float* w, int nout, int nin, std::vector<_Float16>& pk, std::vector<float>& sinv) {
+  if (nin % 16 || nout % 32) throw std::runtime_error("pack_mk_weights: nin % 16 / nout % 32");
+  const int nnt = nout / 32, nks = nin / 16;
+  std::vector<float> scale(nout, 1.f);
+  sinv.assign(nout, 1.f);
+  for (int r = 0; r < nout; ++r) {
+    float amax = 0.f;
+    for (int k = 0; k < nin; ++k) amax = std::max(amax, std::fabs(w[(size_t)r * nin + k]));
+    int e = 0;
+    if (amax > 0.f && std::isfinite(amax)) {
+      int ex;
+      std::frexp(amax, &ex);
+      e = 15 - ex;
+    }
+    scale[r] = std::ldexp(1.0f, e);
+    sinv[r] = std::ldexp(1.0f, -e);
+  }
+  pk.assign((size_t)nnt * nks * 64 * 16, (_Float16)0.f);
+  for (int nt = 0; nt < nnt; ++nt)
+    for (int ks = 0; ks < nks; ++ks)
+      for (int lane = 0; lane < 64; ++lane) {
+        const int col = nt * 32 + (lane & 31);
+        _Float16* dst = pk.data() + (((size_t)nt * nks + ks) * 64 + lane) * 16;
+        for (int e = 0; e < 8; ++e) {
+          const int k = ks * 16 + 8 * (lane >> 5) + e;
+          const float v = w[(size_t)col * nin + k] * scale[col];
+          const _Float16 h = (_Float16)v;
+          dst[e] = h;
+          dst[8 + e] = (_Float16)(v - (float)h);
+        }
+      }
+}
+
+void launch_mk_linear_test(const float* A, int K, const MkLin& W, int N, float* out, hipStream_t st) {
+  if (K % 256 || N % 32 || W.nks != K / 16) throw std::runtime_error("mk_linear_test: K % 256, N % 32");
+  const size_t lds = (size_t)2 * 32 * (K + 8) * 2;
+  DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(mk_linear_test_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(mk_linear_test_kernel, dim3(1), dim3(NT), lds, st, A, K, W, N, out);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
+bool decoder_mk_supported(int Q, int P, int d, int nagents, int Hv, int Wv, int ffn) {
+  return Q == kQ && P == kP && d == kD && nagents == kA && Hv == kHV && Wv == kHV && ffn == kFF;
+}
+
+void launch_decoder_mk(const MkArgs& a, hipStream_t st) {
+  if (a.B <= 0) return;
+  if (!a.dim_t || !a.slots || !a.vrows || !a.akv || !a.ego || !a.film || !a.tfe || !a.pts || !a.imgx)
+    throw std::runtime_error("decoder_mk: missing operand");
+  static bool attr = false;
+  if (!attr) {
+    DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(decoder_mk_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    attr = true;
+  }
+  hipLaunchKernelGGL(decoder_mk_kernel, dim3(a.B), dim3(NT), LDS_BYTES, st, a);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
+void launch_decoder_mk_init(const MkInitArgs& a, hipStream_t st) {
+  if (a.B <= 0) return;
+  hipLaunchKernelGGL(decoder_mk_init_kernel, dim3(a.B), dim3(256), 0, st, a);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ddmi

@@ -5,6 +5,7 @@
 
 #include "../../include/ddmi.h"
 #include "common.h"
+#include "decoder_mk.h"
 #include "weights.h"
 #include <vector>
 
@@ -34,6 +35,28 @@ extern "C" {
 const char* dd_op_last_error(void) { return g_op_err.c_str(); }
 
 const char* dd_op_last_kernel(void) { return last_conv_config(); }
+
+int dd_op_mk_linear(const float* A, int K, const float* wgt, const float* bias, float* out, int N, void* stream) {
+  return op_guard([&] {
+    std::vector<float> hw((size_t)N * K);
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));
+    DD_HIP_CHECK(hipMemcpy(hw.data(), wgt, hw.size() * sizeof(float), hipMemcpyDeviceToHost));
+    std::vector<_Float16> pk;
+    std::vector<float> sinv;
+    pack_mk_weights(hw.data(), N, K, pk, sinv);
+    Arena ar;
+    const size_t wo = ar.add(reinterpret_cast<const float*>(pk.data()), pk.size() / 2);
+    const size_t so = ar.add(sinv);
+    ar.upload();
+    MkLin m;
+    m.w = reinterpret_cast<const uint4*>(ar.ptr(wo));
+    m.s = ar.ptr(so);
+    m.b = bias;
+    m.nks = K / 16;
+    launch_mk_linear_test(A, K, m, N, out, S(stream));
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));
+  });
+}
 
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias, const float* res,
                  float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {

@@ -24,6 +24,7 @@
 
 #include "../../include/ddmi.h"
 #include "common.h"
+#include "decoder_mk.h"
 #include "weights.h"
 
 namespace ddmi {
@@ -52,6 +53,11 @@ struct TfLayerW {
   Lin sa_in, sa_out, ca_q, ca_kv, ca_out, l1, l2;
   LNp n1, n2, n3;
 };
+// a Linear packed for the decoder megakernel (decoder_mk.h MkLin): arena offsets
+struct MkLinOff {
+  size_t w = kNone, s = kNone, b = kNone;
+  int nks = 0;
+};
 struct DiffLayerW {
   Lin attw, outp;
   Conv vproj;
@@ -59,6 +65,7 @@ struct DiffLayerW {
   LNp n1, n2, n3;
   Lin c0, c3, c6, r0, r2, r4;
   LNp c2, c5;
+  MkLinOff m_outp, m_ag_q, m_ag_out, m_ffn0, m_ffn2, m_c0, m_c3, m_r0, m_r2;  // megakernel images
 };
 
 struct KStat {
@@ -129,6 +136,13 @@ class Model {
   bool value_dedup = true;
   // bev_proj's keyval half at 8 x 8 before the upsample (DDMI_BEVPROJ_LOWRES=0: concat at 64 x 64)
   bool bevproj_lowres = true;
+  // f16x3 + gathered value rows: the trajectory head as one megakernel launch per (step, layer)
+  // (decoder_mk.hip; DDMI_DECODER_MK=0: the unfused per-op chain)
+  bool decoder_mk = true;
+  bool mk_ready = false;
+  bool mk_stamps = false;  // diagnostics: per-phase clock stamps of the megakernel (tap "mk_stamps_s*l*")
+  MkLinOff m_pa0, m_pa3;
+  size_t dim_t_off = kNone;
   // graph cache keyed by the forward's shape signature and the buffer generation
   struct GraphEntry {
     hipGraphExec_t exec = nullptr;
@@ -153,6 +167,8 @@ class Model {
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BEVPROJ_LOWRES")) bevproj_lowres = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_DECODER_MK")) decoder_mk = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -355,6 +371,196 @@ class Model {
     }
     bevproj = prep_linear(bx, ar, "bev_proj.0", d, 320);
     bevproj_ln = prep_ln(bx, ar, "bev_proj.2", d);
+    // decoder megakernel images (the reference configuration only)
+    mk_ready = decoder_mk_supported(Q, P, d, 30, cfg.lidar_h / 4, cfg.lidar_w / 4, 1024);
+    if (mk_ready) {
+      for (DiffLayerW& w : dl) {
+        w.m_outp = pack_mk(w.outp);
+        w.m_ag_q = pack_mk(w.ag_q);
+        w.m_ag_out = pack_mk(w.ag_out);
+        w.m_ffn0 = pack_mk(w.ffn0);
+        w.m_ffn2 = pack_mk(w.ffn2);
+        w.m_c0 = pack_mk(w.c0);
+        w.m_c3 = pack_mk(w.c3);
+        w.m_r0 = pack_mk(w.r0);
+        w.m_r2 = pack_mk(w.r2);
+      }
+      m_pa0 = pack_mk(pa0);
+      m_pa3 = pack_mk(pa3);
+      std::vector<float> t(16);
+      for (int j = 0; j < 16; ++j) t[j] = (float)std::pow(10000.0, (double)j / 16.0);  // as decoder.hip
+      dim_t_off = ar.add(t);
+    }
+  }
+
+  // f16x3 image of a Linear in MFMA-fragment order (decoder_mk.h MkLin): the split of prep_split (same
+  // per-output power-of-two scale, hi = f16(w s), lo = f16(w s - hi)), block (nt, ks) = 64 lanes x (8 hi,
+  // 8 lo) halfs, lane = col % 32 + 32 ((k % 16) / 8)
+  MkLinOff pack_mk(const Lin& L) {
+    const std::vector<float> w(ar.host(L.w), ar.host(L.w) + (size_t)L.nout * L.nin);
+    std::vector<_Float16> pk;
+    std::vector<float> sinv;
+    pack_mk_weights(w.data(), L.nout, L.nin, pk, sinv);
+    MkLinOff m;
+    m.w = ar.add(reinterpret_cast<const float*>(pk.data()), pk.size() / 2);
+    m.s = ar.add(sinv);
+    m.b = L.b;
+    m.nks = L.nin / 16;
+    return m;
+  }
+  MkLin mk(const MkLinOff& o) const {
+    MkLin m;
+    m.w = reinterpret_cast<const uint4*>(W(o.w));
+    m.s = W(o.s);
+    m.b = W(o.b);
+    m.nks = o.nks;
+    return m;
+  }
+  MkLayer mk_layer(int l) const {
+    const DiffLayerW& w = dl[l];
+    MkLayer L;
+    L.outp = mk(w.m_outp);
+    L.ag_q = mk(w.m_ag_q);
+    L.ag_out = mk(w.m_ag_out);
+    L.ffn0 = mk(w.m_ffn0);
+    L.ffn2 = mk(w.m_ffn2);
+    L.c0 = mk(w.m_c0);
+    L.c3 = mk(w.m_c3);
+    L.r0 = mk(w.m_r0);
+    L.r2 = mk(w.m_r2);
+    L.attw_w = W(w.attw.w);
+    L.attw_b = W(w.attw.b);
+    L.c6_w = W(w.c6.w);
+    L.c6_b = W(w.c6.b);
+    L.r4_w = W(w.r4.w);
+    L.r4_b = W(w.r4.b);
+    L.n1g = W(w.n1.g);
+    L.n1b = W(w.n1.b);
+    L.n2g = W(w.n2.g);
+    L.n2b = W(w.n2.b);
+    L.n3g = W(w.n3.g);
+    L.n3b = W(w.n3.b);
+    L.c2g = W(w.c2.g);
+    L.c2b = W(w.c2.b);
+    L.c5g = W(w.c5.g);
+    L.c5b = W(w.c5.b);
+    return L;
+  }
+
+  // value_proj (3x3 conv 256 -> 256 + ReLU, blocks.py:68-76,114) of layer l evaluated only at the map
+  // pixels the (step, layer)'s taps read: conv_x3 over the deduplicated row list `rows`
+  void gathered_value(int l, const int* rows, float* vrows, const float* cross, int B, int HB, int WB, int MR) {
+    const int d = 256;
+    ConvArgs a = conv_args(dl[l].vproj, cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, B, HB, WB, vrows,
+                           (int64_t)MR * d, d, 0, true, nullptr, 0, 0, 0);
+    a.Nimg = 1;
+    a.Ho = MR;
+    a.Wo = 1;
+    a.rowmap = rows;
+    a.rowmap_nimg = B;
+    const double fl = 2.0 * MR * (double)d * 9 * dl[l].vproj.cin_real;
+    launch("conv_x3", fl, [&] { launch_conv_gemm(a, st); }, &a);
+  }
+
+  // TrajectoryHead.forward_test (:578-641) as 1 + 2 x steps x 2 launches: the DDIM start + first taps, then
+  // per (step, layer) the gathered value_proj conv and the decoder megakernel (decoder_mk.hip)
+  void traj_head_mk(int B, int steps, const float* cross, float* const akv[2], float* const egos[2],
+                    bool& tf_pending, const float* noise) {
+    const int d = 256, Q = cfg.num_modes, P = cfg.num_poses, R = B * Q;
+    const int HB = cfg.lidar_h / 4, WB = cfg.lidar_w / 4, MR = R * P * 4;
+    const bool vanilla = schedule == DD_SCHED_VANILLA;
+    const std::vector<int> roll = denoise_timesteps(steps);
+    const int ratio = vanilla ? 1000 / steps : 1;
+    auto sfx = [](int s, int l) { return "_s" + std::to_string(s) + "l" + std::to_string(l); };
+    auto rows_of = [&](int s, int l) { return reinterpret_cast<int*>(buf("value_taps" + sfx(s, l), (size_t)MR)); };
+    auto slots_of = [&](int s, int l) { return reinterpret_cast<int*>(buf("value_slots" + sfx(s, l), (size_t)MR)); };
+    float* imgx = buf("ddim_img", (size_t)R * P * 2);
+    float* tfe = buf("traj_feature", (size_t)R * d);
+    float* pts = buf("pts", (size_t)R * P * 2);
+    float* pts2 = buf("pts_next", (size_t)R * P * 2);
+    float* traj = buf("trajectory", (size_t)B * P * 3);
+    int* idx = reinterpret_cast<int*>(buf("mode_idx", B));
+    {
+      // truncated: add_noise(norm_odo(anchor), noise, t = trunc_timestep) (:593-597);
+      // vanilla (C5 ablation): x_T = noise (sa = 0, s1a = 1 keep it bit-exact)
+      const float a8 = ac[cfg.trunc_timestep];
+      MkInitArgs ia;
+      ia.anchor = W(anchor);
+      ia.noise = noise;
+      ia.imgx = imgx;
+      ia.rows = rows_of(0, 0);
+      ia.slots = slots_of(0, 0);
+      ia.sa = vanilla ? 0.0f : std::sqrt(a8);
+      ia.s1a = vanilla ? 1.0f : std::sqrt(1.0f - a8);
+      ia.B = B;
+      launch("decoder", 0, [&] { launch_decoder_mk_init(ia, st); });
+    }
+    const MkLayer layers[2] = {mk_layer(0), mk_layer(1)};
+    MkAnchor anc;
+    anc.pa0 = mk(m_pa0);
+    anc.pa3 = mk(m_pa3);
+    anc.pa2g = W(pa2.g);
+    anc.pa2b = W(pa2.b);
+    float* reg_last = nullptr;
+    float* cls_last = nullptr;
+    for (int si = 0; si < steps; ++si) {
+      for (int l = 0; l < 2; ++l) {
+        const std::string sf = sfx(si, l);
+        float* vrows = buf("value_rows" + sf, (size_t)MR * d);
+        gathered_value(l, rows_of(si, l), vrows, cross, B, HB, WB, MR);
+        if (tf_pending) {
+          join();  // tf decoder: agent K / V and ego rows of both layers
+          tf_pending = false;
+        }
+        MkArgs m;
+        m.L = layers[l];
+        m.A = anc;
+        m.layer = l;
+        m.B = B;
+        m.imgx = imgx;
+        m.tfe = tfe;
+        m.pts = l == 0 ? pts : pts2;
+        m.pts_next = l == 0 ? pts2 : nullptr;
+        m.vrows = vrows;
+        m.slots = slots_of(si, l);
+        m.akv = akv[l];
+        m.ego = egos[l];
+        m.film = buf("film_s" + std::to_string(si) + "l" + std::to_string(l), 2 * d);
+        m.gs_out = buf("gs" + sf, (size_t)R * d);
+        m.reg_out = buf("reg" + sf, (size_t)R * P * 3);
+        m.cls_out = buf("cls" + sf, R);
+        if (l == 0) {
+          m.next_rows = rows_of(si, 1);
+          m.next_slots = slots_of(si, 1);
+        } else if (si + 1 < steps) {
+          m.next_rows = rows_of(si + 1, 0);
+          m.next_slots = slots_of(si + 1, 0);
+          const int k = roll[si];
+          const float a_t = ac[k], a_p = (k - ratio >= 0) ? ac[k - ratio] : 1.0f;
+          m.ddim = 1;
+          m.sa_t = std::sqrt(a_t);
+          m.sb_t = std::sqrt(1.0f - a_t);
+          m.sa_p = std::sqrt(a_p);
+          m.sdir = std::sqrt(1.0f - a_p);
+        } else {
+          m.traj = traj;
+          m.mode_idx = idx;
+        }
+        m.flags = num_flags;
+        m.dim_t = W(dim_t_off);
+        if (mk_stamps) m.stamps = reinterpret_cast<unsigned long long*>(buf("mk_stamps" + sf, (size_t)B * 80));
+        // algorithmic FLOPs of the launch: the 256-wide Linears (+ the anchor encoder at layer 0) and the
+        // fp32 heads, 2 x rows x sum(K x N)
+        double kn = 7.0 * d * d + 2.0 * d * 1024 + (double)d * (P + 1 + 3 * P);
+        if (l == 0) kn += 512.0 * d + (double)d * d;
+        launch("decoder", 2.0 * R * kn, [&] { launch_decoder_mk(m, st); });
+        reg_last = m.reg_out;
+        cls_last = m.cls_out;
+      }
+    }
+    join();  // the heads branch on the side stream
+    alias("poses_reg", reg_last);
+    alias("poses_cls", cls_last);
   }
 
   // ------------------------------------------------------------------ runtime helpers
@@ -939,6 +1145,10 @@ class Model {
     });
 
     // ---- trajectory head (TrajectoryHead.forward_test, :578-641)
+    if (decoder_mk && mk_ready && gathered) {
+      traj_head_mk(B, steps, cross, akv, egos, tf_pending, noise);
+      return;
+    }
     float* imgx = buf("ddim_img", (size_t)R * P * 2);
     const bool vanilla = schedule == DD_SCHED_VANILLA;
     {

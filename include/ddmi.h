@@ -147,6 +147,9 @@ const char* dd_op_last_error(void);
 /* Kernel and tile configuration of the calling thread's last conv / GEMM launch (dd_op_* or forward), e.g.
  * "conv_x6<8,32,128,4,2>": lets tests prove which route a shape took. */
 const char* dd_op_last_kernel(void);
+/* The decoder megakernel's GEMM core (decoder_mk.hip): out[32][N] = A[32][K] W^T + bias, A and W fp32 (W
+ * [N][K] packed on the host into the MFMA-fragment f16x3 image), K % 256 == 0, N % 32 == 0; synchronous. */
+int dd_op_mk_linear(const float* A, int K, const float* wgt, const float* bias, float* out, int N, void* stream);
 /* NHWC conv: in (B,H,W,Cin), wgt (Cout,KH,KW,Cin), optional bias (Cout), res (B,Ho,Wo,Cout). */
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
                  const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream);

@@ -389,3 +389,17 @@ def test_stem_pool_f16x3(gpu, B, H, W):
                               flags.data_ptr(), None), gpu)
     close(out.permute(0, 3, 1, 2), ref, 3e-5)
     assert int(flags.item()) == 0
+
+
+@pytest.mark.parametrize("K,N", [(256, 256), (512, 256), (256, 1024), (1024, 256)])
+def test_mk_linear_core(gpu, K, N):
+    """The decoder megakernel's GEMM core (LDS split + fragment-order f16x3 weights + 32x32x16 MFMA) vs
+    PyTorch fp64: 32 rows, fp32-class tolerance."""
+    a = rnd(32, K, seed=91)
+    w = rnd(N, K, seed=92, scale=1.0 / np.sqrt(K))
+    b = rnd(N, seed=93)
+    ref = a.double() @ w.double().T + b.double()
+    out = torch.empty(32, N, device=DEV)
+    ad, wd, bd = g(a), g(w), g(b)
+    ok(gpu.dd_op_mk_linear(ad.data_ptr(), K, wd.data_ptr(), bd.data_ptr(), out.data_ptr(), N, None), gpu)
+    close(out, ref, 3e-5)
