@@ -20,7 +20,7 @@ ARCH = os.environ.get("DDMI_ARCH", "gfx950")
 # megakernel records per-phase clock stamps (tools/debug/mk_stamps.py); the product library has none
 VARIANT = os.environ.get("DDMI_BUILD_VARIANT", "")
 LIB = os.path.join(HERE, "libddmi.so" if not VARIANT else f"libddmi_{VARIANT}.so")
-VARIANT_FLAGS = {"": [], "stamps": ["-DDDMI_MK_STAMPS"]}[VARIANT]
+VARIANT_FLAGS = {"": [], "stamps": ["-DDDMI_MK_STAMPS"], "nopv": ["-DDDMI_MK_STAMPS", "-DDDMI_MK_NOPV"]}[VARIANT]
 SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "decoder_mk.hip", "attention.hip", "stem_pool.hip", "features.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", CSRC, "-I", INCLUDE] + VARIANT_FLAGS

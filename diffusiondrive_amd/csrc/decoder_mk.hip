@@ -60,7 +60,8 @@ constexpr int S_PN = S_PTS + 2 * kQP;   // [160][2] next points
 constexpr int S_RR = S_PN + 2 * kQP;    // [20][24] reg head raw
 constexpr int S_REG = S_RR + kQ * 24;   // [160][3] reg output
 constexpr int S_CLS = S_REG + 3 * kQP;  // [20] cls logits
-constexpr int S_END = S_CLS + 32;
+constexpr int S_SLOT = S_CLS + 32;      // [160] int4 tap slots of this (step, layer), staged at the start
+constexpr int S_END = S_SLOT + 4 * kQP;
 constexpr int LDS_BYTES = OFF_SMALL + S_END * 4;
 static_assert(2 * 32 * HP2 * 2 <= 4 * SPLIT_BYTES, "K = 512 operand fits the two split buffers");
 static_assert(kA * 2 * kD * 4 <= 4 * SPLIT_BYTES, "agent K / V fit the two split buffers");
@@ -117,16 +118,25 @@ __device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int*
   const int E = (HW + nt - 1) / nt;
   int cnt = 0;
   for (int e = tid * E; e < min(HW, tid * E + E); ++e) cnt += table[e];
-  scan[tid] = cnt;
-  __syncthreads();
-  for (int off = 1; off < nt; off <<= 1) {
-    const int v = tid >= off ? scan[tid - off] : 0;
-    __syncthreads();
-    scan[tid] += v;
-    __syncthreads();
+  // exclusive prefix of the per-thread counts: inclusive wave scan by shuffles, then the wave totals
+  const int lane = tid & 63, wv = tid >> 6, nw = (nt + 63) >> 6;
+  int inc = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
   }
+  if (lane == 63) scan[wv] = inc;
+  __syncthreads();
+  int wbase = 0, total = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int t = scan[w];
+    if (w < wv) wbase += t;
+    total += t;
+  }
+  __syncthreads();  // scan[] is free again (the caller's table + 4096 stays untouched otherwise)
+  scan[tid] = wbase + inc;  // inclusive prefix, as the rest of the function expects
   int r = scan[tid] - cnt;
-  const int total = scan[nt - 1];
   for (int e = tid * E; e < min(HW, tid * E + E); ++e)
     if (table[e]) {
       table[e] = r;
@@ -154,34 +164,55 @@ __device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int*
 // acc += A[32][aks*16 .. (aks+NKS)*16) (split LDS images, row pitch hp halfs) x W[:, wks*16 ..]^T for
 // the 32 output columns of tile nt: the NKS fragment pairs of the wave are loaded first (2 KB contiguous
 // per fragment per wave), then 3 f16 MFMAs per k16 step (small terms first, as conv_x3)
-template <int NKS>
-__device__ inline void mk_gemm(const char* ahi, const char* alo, int hp, const MkLin& L, int nt, int wks,
-                               mk_f16& acc, int aks = 0) {
-  // a ring of PF fragment pairs in flight (PF x 32 B per lane); fence the scheduler at both ends so the
-  // next GEMM's loads are not hoisted into this one (their registers would not fit beside these)
-  constexpr int PF = 8;
-  static_assert(NKS % PF == 0, "ring");
-  __builtin_amdgcn_sched_barrier(0);
-  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
-  const uint4* wb = L.w + ((size_t)(nt * L.nks + wks) * 64 + lane) * 2;
-  uint4 bh[PF], bl[PF];
+// The B (weight) fragments stream through a ring of PF fragment pairs per wave (PF x 32 B per lane). A GEMM
+// starts with its first PF steps already in the ring and, as its last PF steps free their slots, loads the
+// first PF steps of the NEXT GEMM (`nx`, tile nnt, k-step nwks), so those loads fly under this GEMM's tail,
+// its epilogue, the barrier and whatever LDS / VALU phase separates the two GEMMs.
+constexpr int PF = 8;
+struct Ring {
+  uint4 h[PF], l[PF];
+};
+
+__device__ inline const uint4* mk_wbase(const MkLin& L, int nt, int wks) {
+  return L.w + ((size_t)(nt * L.nks + wks) * 64 + (threadIdx.x & 63)) * 2;
+}
+
+__device__ inline void ring_fill(Ring& R, const MkLin& L, int nt, int wks) {
+  const uint4* wb = mk_wbase(L, nt, wks);
 #pragma unroll
   for (int s = 0; s < PF; ++s) {
-    bh[s] = wb[s * 128];
-    bl[s] = wb[s * 128 + 1];
+    R.h[s] = wb[s * 128];
+    R.l[s] = wb[s * 128 + 1];
   }
+}
+
+// acc += A[32][aks*16 .. (aks+NKS)*16) (split LDS images, row pitch hp halfs) x W[:, wks*16 ..]^T for the 32
+// output columns of tile nt, 3 f16 MFMAs per k16 step (small terms first, as conv_x3); R holds this GEMM's
+// first PF steps on entry and the next GEMM's (nx) on exit (nx.w == nullptr: nothing next)
+template <int NKS>
+__device__ inline void mk_gemm(const char* ahi, const char* alo, int hp, const MkLin& L, int nt, int wks, mk_f16& acc,
+                               int aks, Ring& R, const MkLin& nx, int nnt, int nwks) {
+  static_assert(NKS % PF == 0 && NKS >= PF, "ring");
+  __builtin_amdgcn_sched_barrier(0);
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  const uint4* wb = mk_wbase(L, nt, wks);
+  const uint4* nb = nx.w ? mk_wbase(nx, nnt, nwks) : nullptr;
   const int aoff = li * hp * 2 + hh * 16 + aks * 32;
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
     const mk_h8 ah = *reinterpret_cast<const mk_h8*>(ahi + aoff + s * 32);
     const mk_h8 al = *reinterpret_cast<const mk_h8*>(alo + aoff + s * 32);
-    const mk_h8 wh = __builtin_bit_cast(mk_h8, bh[s % PF]), wl = __builtin_bit_cast(mk_h8, bl[s % PF]);
+    const mk_h8 wh = __builtin_bit_cast(mk_h8, R.h[s % PF]), wl = __builtin_bit_cast(mk_h8, R.l[s % PF]);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wh, acc, 0, 0, 0);
     if (s + PF < NKS) {
-      bh[s % PF] = wb[(s + PF) * 128];
-      bl[s % PF] = wb[(s + PF) * 128 + 1];
+      R.h[s % PF] = wb[(s + PF) * 128];
+      R.l[s % PF] = wb[(s + PF) * 128 + 1];
+    } else if (nb) {
+      const int t = s + PF - NKS;
+      R.h[s % PF] = nb[t * 128];
+      R.l[s % PF] = nb[t * 128 + 1];
     }
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -279,6 +310,11 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   auto stamp = [](int) {};
 #endif
   stamp(0);
+  const MkLin none{};
+  Ring R;
+  ring_fill(R, a.layer == 0 ? a.A.pa0 : L.outp, wave, 0);  // flies under the prologue
+  int4* SLOT = reinterpret_cast<int4*>(SM + S_SLOT);
+  for (int t = tid; t < kQP; t += NT) SLOT[t] = reinterpret_cast<const int4*>(a.slots)[(int64_t)b * kQP + t];
 
   // ================================================================ layer 0: points, embedding, anchor encoder
   if (a.layer == 0) {
@@ -303,27 +339,29 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
       const float u = ((f < 16) ? SM[S_PTS + 2 * t + 1] : SM[S_PTS + 2 * t]) * 6.283185307179586f;
       const float ang = u / dim_t[f & 15];
       const int col = p * 64 + 2 * f;
-      st_split(EH, HP2, q, col, sinf(ang));
-      st_split(EH, HP2, q, col + 1, cosf(ang));
+      float sn, cs;
+      sincosf(ang, &sn, &cs);  // one range reduction for the pair (the arguments reach ~380 rad)
+      st_split(EH, HP2, q, col, sn);
+      st_split(EH, HP2, q, col + 1, cs);
     }
     for (int e = tid; e < (32 - kQ) * 512; e += NT) st_split(EH, HP2, kQ + (e >> 9), e & 511, 0.f);
     __syncthreads();
     mk_f16 acc;
     zero_acc(acc);
-    mk_gemm<16>(EH, EH + 32 * HP2 * 2, HP2, a.A.pa0, wave, 0, acc);
-    mk_gemm<16>(EH, EH + 32 * HP2 * 2, HP2, a.A.pa0, wave, 16, acc, 16);
+    mk_gemm<32>(EH, EH + 32 * HP2 * 2, HP2, a.A.pa0, wave, 0, acc, 0, R, a.A.pa3, wave, 0);
     mk_epi(acc, a.A.pa0, wave, a.flags, [&](int row, int col, float v) { T1[row * FP + col] = fmaxf(v, 0.f); });
     __syncthreads();
     stamp(2);
-    for (int q = wave; q < 32; q += 8) {
-      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (q < kQ) o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], a.A.pa2g, a.A.pa2b, lane);
-      st_split4(SA, HP, q, lane * 4, o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = wave + 8 * k;
+      const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], a.A.pa2g, a.A.pa2b, lane);
+      st_split4(SA, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
     }
     __syncthreads();
     stamp(3);
     zero_acc(acc);
-    mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, a.A.pa3, wave, 0, acc);
+    mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, a.A.pa3, wave, 0, acc, 0, R, L.outp, wave, 0);
     mk_epi(acc, a.A.pa3, wave, a.flags, [&](int row, int col, float v) {
       if (row < kQ) {
         X1[row * FP + col] = v;
@@ -345,75 +383,77 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   stamp(4);
 
   // ================================================================ GridSampleCrossBEVAttention
-  // logits = attention_weights(query) (Linear 256 -> 8, fp32), softmax over the 8 points: a wave per
-  // query, a float4 of channels per lane (the 8 weight rows held in registers), wave reductions
+  // logits = attention_weights(query) (Linear 256 -> 8, fp32), softmax over the 8 points: the 8 weight
+  // rows staged in LDS (SB is free here), a thread per (query, point) walking the two rows in LDS
   {
-    float4 wr[kP];
-#pragma unroll
-    for (int p = 0; p < kP; ++p) wr[p] = reinterpret_cast<const float4*>(L.attw_w + p * kD)[lane];
-    for (int q = wave; q < kQ; q += 8) {
-      const float4 x = reinterpret_cast<const float4*>(X1 + q * FP)[lane];
-      float lg[kP];
-#pragma unroll
-      for (int p = 0; p < kP; ++p)
-        lg[p] = wave_sum((x.x * wr[p].x + x.y * wr[p].y) + (x.z * wr[p].z + x.w * wr[p].w)) + L.attw_b[p];
+    float* AW = reinterpret_cast<float*>(SB);  // [8][FP]: padded rows, conflict-free across points
+    for (int e = tid; e < kP * kD / 4; e += NT)
+      *reinterpret_cast<float4*>(AW + (e >> 6) * FP + (e & 63) * 4) = reinterpret_cast<const float4*>(L.attw_w)[e];
+    __syncthreads();
+    if (tid < kQP) {
+      const int q = tid >> 3, p = tid & 7;
+      const float4* xr = reinterpret_cast<const float4*>(X1 + q * FP);
+      const float4* wr = reinterpret_cast<const float4*>(AW + p * FP);
+      float s0 = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < kD / 4; ++c) {
+        const float4 x = xr[c], w = wr[c];
+        s0 += x.x * w.x;
+        s0 += x.y * w.y;
+        s0 += x.z * w.z;
+        s0 += x.w * w.w;
+      }
+      SM[S_W8 + tid] = s0 + L.attw_b[p];
+    }
+    __syncthreads();
+    if (tid < kQ) {
+      float* w = SM + S_W8 + tid * kP;
       float mx = -INFINITY;
-#pragma unroll
-      for (int p = 0; p < kP; ++p) mx = fmaxf(mx, lg[p]);
-      float s = 0.f;
-#pragma unroll
+      for (int p = 0; p < kP; ++p) mx = fmaxf(mx, w[p]);
+      float e[kP], sm = 0.f;
       for (int p = 0; p < kP; ++p) {
-        lg[p] = expf(lg[p] - mx);
-        s += lg[p];
+        e[p] = expf(w[p] - mx);
+        sm += e[p];
       }
-      const float inv = 1.f / s;
-      if (lane < kP) {
-        float v = 0.f;
-#pragma unroll
-        for (int p = 0; p < kP; ++p) v = lane == p ? lg[p] * inv : v;
-        SM[S_W8 + q * kP + lane] = v;
-      }
+      const float inv = 1.f / sm;
+      for (int p = 0; p < kP; ++p) w[p] = e[p] * inv;
     }
   }
   __syncthreads();
-  stamp(5);
   // sum_p w_p * bilinear(value, point p): one wave per query, a float4 of channels per lane; the value
   // rows are the gathered value_proj rows of the scene's distinct tap pixels (slots)
   for (int q = wave; q < 32; q += 8) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (q < kQ) {
+      int4 sl[kP];
 #pragma unroll
-      for (int g = 0; g < kP; g += 2) {
-        float4 v[2][4];
-        float wt[2][4];
-        bool ok[2][4];
+      for (int p = 0; p < kP; ++p) sl[p] = SLOT[q * kP + p];
 #pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
-          const int t = q * kP + g + pp;
-          int x0, y0;
-          tap_geom(SM[S_PTS + 2 * t], SM[S_PTS + 2 * t + 1], x0, y0, wt[pp]);
-          const int4 sl = *reinterpret_cast<const int4*>(a.slots + ((int64_t)b * kQP + t) * 4);
-          const int sv[4] = {sl.x, sl.y, sl.z, sl.w};
+      for (int g = 0; g < kP; g += 4) {
+        float4 v[4][4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            ok[pp][u] = sv[u] >= 0;  // slot -1 <=> the tap reads zero padding
-            v[pp][u] = ok[pp][u] ? *reinterpret_cast<const float4*>(a.vrows + (int64_t)sv[u] * kD + lane * 4)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
+        for (int pp = 0; pp < 4; ++pp) {
+          const int sv[4] = {sl[g + pp].x, sl[g + pp].y, sl[g + pp].z, sl[g + pp].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)  // slot -1 <=> the tap reads zero padding
+            v[pp][u] = sv[u] >= 0 ? *reinterpret_cast<const float4*>(a.vrows + (int64_t)sv[u] * kD + lane * 4)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
+        for (int pp = 0; pp < 4; ++pp) {
+          const int t = q * kP + g + pp;
+          int x0, y0;
+          float wt[4];
+          tap_geom(SM[S_PTS + 2 * t], SM[S_PTS + 2 * t + 1], x0, y0, wt);
           float4 sp = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            if (ok[pp][u]) {
-              sp.x += v[pp][u].x * wt[pp][u];
-              sp.y += v[pp][u].y * wt[pp][u];
-              sp.z += v[pp][u].z * wt[pp][u];
-              sp.w += v[pp][u].w * wt[pp][u];
-            }
+            sp.x += v[pp][u].x * wt[u];
+            sp.y += v[pp][u].y * wt[u];
+            sp.z += v[pp][u].z * wt[u];
+            sp.w += v[pp][u].w * wt[u];
           }
-          const float wp = SM[S_W8 + q * kP + g + pp];
+          const float wp = SM[S_W8 + t];
           acc.x += wp * sp.x;
           acc.y += wp * sp.y;
           acc.z += wp * sp.z;
@@ -429,7 +469,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // output_proj + residual (blocks.py:127-129): x1 = W gso + b + query
   mk_f16 acc;
   zero_acc(acc);
-  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.outp, wave, 0, acc);
+  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.outp, wave, 0, acc, 0, R, L.ag_q, wave, 0);
   mk_epi(acc, L.outp, wave, a.flags, [&](int row, int col, float v) {
     float x = 0.f;
     if (row < kQ) {
@@ -443,7 +483,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
 
   // ================================================================ cross_agent_attention (+ norm1)
   zero_acc(acc);
-  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ag_q, wave, 0, acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ag_q, wave, 0, acc, 0, R, L.ag_out, wave, 0);
   mk_epi(acc, L.ag_q, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) T1[row * FP + col] = v;
   });
@@ -508,7 +548,12 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     float o[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) o[d] = 0.f;
+#ifdef DDMI_MK_NOPV
+    for (int j = 0; j < 0; ++j) {
+#else
+#pragma unroll 6
     for (int j = 0; j < kA; ++j) {
+#endif
       const float pj = pr[j];
       const float* vr = KV + j * 2 * kD + kD + h * kHD + half * 16;
 #pragma unroll
@@ -525,25 +570,26 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   stamp(13);
   // out_proj + residual
   zero_acc(acc);
-  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ag_out, wave, 0, acc);
+  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ag_out, wave, 0, acc, 0, R, L.ffn0, wave, 0);
   mk_epi(acc, L.ag_out, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) X1[row * FP + col] = v + X1[row * FP + col];
   });
   __syncthreads();
   stamp(14);
   // norm1; cross_ego_attention over one key = the hoisted ego row, residual; norm2 -> FFN operand
-  for (int q = wave; q < 32; q += 8) {
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q < kQ) {
+  {
+    const float4 eg = reinterpret_cast<const float4*>(a.ego + (int64_t)b * kD)[lane];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // rows 20..31 compute garbage that is never stored
+      const int q = wave + 8 * k;
       float4 v = ln256(reinterpret_cast<const float4*>(X1 + q * FP)[lane], L.n1g, L.n1b, lane);
-      const float4 eg = reinterpret_cast<const float4*>(a.ego + (int64_t)b * kD)[lane];
       v.x += eg.x;
       v.y += eg.y;
       v.z += eg.z;
       v.w += eg.w;
-      o = ln256(v, L.n2g, L.n2b, lane);
+      const float4 o = ln256(v, L.n2g, L.n2b, lane);
+      st_split4(SB, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
     }
-    st_split4(SB, HP, q, lane * 4, o);
   }
   __syncthreads();
   stamp(15);
@@ -553,12 +599,14 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   zero_acc(acc2);
   for (int c = 0; c < kFF / kD; ++c) {
     zero_acc(acc);
-    mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ffn0, c * 8 + wave, 0, acc);
+    mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ffn0, c * 8 + wave, 0, acc, 0, R, L.ffn2, wave, c * 16);
     mk_epi(acc, L.ffn0, c * 8 + wave, a.flags,
            [&](int row, int col, float v) { st_split(SA, HP, row, col - c * kD, row < kQ ? fmaxf(v, 0.f) : 0.f); });
     __syncthreads();
     stamp(16 + 2 * c);
-    mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ffn2, wave, c * 16, acc2);
+    const bool more = c + 1 < kFF / kD;
+    mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ffn2, wave, c * 16, acc2, 0, R, more ? L.ffn0 : L.c0,
+                more ? (c + 1) * 8 + wave : wave, 0);
     __syncthreads();
     stamp(17 + 2 * c);
   }
@@ -567,79 +615,92 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   });
   __syncthreads();
   stamp(24);
-  for (int q = wave; q < 32; q += 8) {
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q < kQ) {
-      o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.n3g, L.n3b, lane);
-      const float4 fs = reinterpret_cast<const float4*>(a.film)[lane];
-      const float4 fb = reinterpret_cast<const float4*>(a.film + kD)[lane];
+  {
+    const float4 fs = reinterpret_cast<const float4*>(a.film)[lane];
+    const float4 fb = reinterpret_cast<const float4*>(a.film + kD)[lane];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = wave + 8 * k;
+      float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.n3g, L.n3b, lane);
       o.x = o.x * (1.f + fs.x) + fb.x;
       o.y = o.y * (1.f + fs.y) + fb.y;
       o.z = o.z * (1.f + fs.z) + fb.z;
       o.w = o.w * (1.f + fs.w) + fb.w;
+      st_split4(SB, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
     }
-    st_split4(SB, HP, q, lane * 4, o);
   }
   __syncthreads();
   stamp(25);
 
   // ================================================================ task decoder: cls and reg branches
   zero_acc(acc);
-  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c0, wave, 0, acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c0, wave, 0, acc, 0, R, L.r0, wave, 0);
   mk_epi(acc, L.c0, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
   });
   zero_acc(acc);
-  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.r0, wave, 0, acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.r0, wave, 0, acc, 0, R, L.c3, wave, 0);
   mk_epi(acc, L.r0, wave, a.flags, [&](int row, int col, float v) { st_split(SA, HP, row, col, row < kQ ? fmaxf(v, 0.f) : 0.f); });
   __syncthreads();
   stamp(26);
-  for (int q = wave; q < 32; q += 8) {
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q < kQ) o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c2g, L.c2b, lane);
-    st_split4(SB, HP, q, lane * 4, o);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int q = wave + 8 * k;
+    const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c2g, L.c2b, lane);
+    st_split4(SB, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
   }
   __syncthreads();
   stamp(27);
   zero_acc(acc);
-  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c3, wave, 0, acc);
+  mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c3, wave, 0, acc, 0, R, L.r2, wave, 0);
   mk_epi(acc, L.c3, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
   });
   zero_acc(acc);
-  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.r2, wave, 0, acc);
+  mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.r2, wave, 0, acc, 0, R, none, 0, 0);
   mk_epi(acc, L.r2, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) X1[row * FP + col] = fmaxf(v, 0.f);
   });
   __syncthreads();
   stamp(28);
   // cls: LN, Linear 256 -> 1 (a wave per query); reg: Linear 256 -> 24 (a thread per output)
-  for (int q = wave; q < kQ; q += 8) {
-    const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c5g, L.c5b, lane);
+  {
     const float4 w = reinterpret_cast<const float4*>(L.c6_w)[lane];
-    const float s = wave_sum((o.x * w.x + o.y * w.y) + (o.z * w.z + o.w * w.w));
-    if (lane == 0) {
-      const float c = s + L.c6_b[0];
-      SM[S_CLS + q] = c;
-      a.cls_out[row0 + q] = c;
-    }
-  }
-  for (int h = 0; h < 2; ++h) {
-    constexpr int NO = kP * 3 / 2;
-    float4 wr[NO];
 #pragma unroll
-    for (int o = 0; o < NO; ++o) wr[o] = reinterpret_cast<const float4*>(L.r4_w + (h * NO + o) * kD)[lane];
-    for (int q = wave; q < kQ; q += 8) {
-      const float4 x = reinterpret_cast<const float4*>(X1 + q * FP)[lane];
-#pragma unroll
-      for (int o = 0; o < NO; ++o) {
-        const float s = wave_sum((x.x * wr[o].x + x.y * wr[o].y) + (x.z * wr[o].z + x.w * wr[o].w));
-        if (lane == 0) SM[S_RR + q * kP * 3 + h * NO + o] = s + L.r4_b[h * NO + o];
+    for (int k = 0; k < 3; ++k) {  // queries wave, wave + 8, wave + 16 (< 20 when wave < 4)
+      const int q = wave + 8 * k;
+      const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c5g, L.c5b, lane);
+      const float s = wave_sum((o.x * w.x + o.y * w.y) + (o.z * w.z + o.w * w.w));
+      if (lane == 0 && q < kQ) {
+        const float c = s + L.c6_b[0];
+        SM[S_CLS + q] = c;
+        a.cls_out[row0 + q] = c;
       }
     }
   }
+
+  {
+    float* RW = reinterpret_cast<float*>(SA);  // r4 weights [24][FP]: padded rows, conflict-free across outputs
+    for (int e = tid; e < kP * 3 * kD / 4; e += NT)
+      *reinterpret_cast<float4*>(RW + (e >> 6) * FP + (e & 63) * 4) = reinterpret_cast<const float4*>(L.r4_w)[e];
+    __syncthreads();
+    if (tid < kQ * kP * 3) {
+      const int q = tid / (kP * 3), o = tid - q * (kP * 3);
+      const float4* xr = reinterpret_cast<const float4*>(X1 + q * FP);
+      const float4* wr = reinterpret_cast<const float4*>(RW + o * FP);
+      float s0 = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < kD / 4; ++c) {
+        const float4 x = xr[c], w = wr[c];
+        s0 += x.x * w.x;
+        s0 += x.y * w.y;
+        s0 += x.z * w.z;
+        s0 += x.w * w.w;
+      }
+      SM[S_RR + tid] = s0 + L.r4_b[o];
+    }
+  }
   __syncthreads();
-  stamp(29);
   // reg[..., :2] += points; reg[..., 2] = tanh * pi (transfuser_model_v2.py:376-380)
   for (int t = tid; t < kQP; t += NT) {
     const float* rr = SM + S_RR + t * 3;
@@ -734,10 +795,14 @@ __global__ __launch_bounds__(NT, 1) void mk_linear_test_kernel(const float* __re
   const int hp = K + 8;
   for (int e = tid; e < 32 * K; e += NT) st_split(lds, hp, e / K, e % K, A[e]);
   __syncthreads();
+  const MkLin none{};
   for (int nt = wave; nt < N / 32; nt += 8) {
     mk_f16 acc;
     zero_acc(acc);
-    for (int ks = 0; ks < K / 16; ks += 16) mk_gemm<16>(lds, lds + 32 * hp * 2, hp, W, nt, ks, acc, ks);
+    Ring R;
+    ring_fill(R, W, nt, 0);
+    for (int ks = 0; ks < K / 16; ks += 16)
+      mk_gemm<16>(lds, lds + 32 * hp * 2, hp, W, nt, ks, acc, ks, R, ks + 16 < K / 16 ? W : none, nt, ks + 16);
     mk_epi(acc, W, nt, nullptr, [&](int row, int col, float v) { out[row * N + col] = v; });
   }
 }

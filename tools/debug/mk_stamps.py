@@ -17,15 +17,16 @@ nz = torch.from_numpy(inp["noise"]).cuda()
 for _ in range(4):
     m.forward(feats, noise=nz)
 torch.cuda.synchronize()
-LABELS = ["start", "pts", "emb", "pa0", "ln+pa3", "logits", "sample", "outp", "ag_q", "kv", "qload", "scores",
-          "pv", "split", "ag_out", "ln12"] + [f"ffn{c}{h}" for c in range(4) for h in "ab"] + [
-          "ffn_epi", "ln3", "c0r0", "lnc2", "c3r2", "heads", "final", "ddim", "end"]
+LABELS = {1: "pts", 2: "emb", 3: "pa0", 4: "ln+pa3", 6: "logits+sample", 7: "outp", 8: "ag_q", 9: "kv",
+          10: "qload", 11: "scores", 12: "pv", 13: "split", 14: "ag_out", 15: "ln12", 24: "ffn_epi", 25: "ln3",
+          26: "c0r0", 27: "lnc2", 28: "c3r2", 30: "heads", 31: "final+ddim", 32: "end"}
+LABELS.update({16 + 2 * c + h: f"ffn{c}{'ab'[h]}" for c in range(4) for h in range(2)})
 for s in range(2):
     for l in range(2):
         st = m.tap(f"mk_stamps_s{s}l{l}").cpu().numpy().view(np.uint64)[: B * 40].reshape(B, 40).astype(np.int64)
         live = [k for k in range(40) if (st[:, k] > 0).all()]
         parts = []
         for a_, b_ in zip(live[:-1], live[1:]):
-            parts.append(f"{LABELS[b_]}={int(np.median(st[:, b_] - st[:, a_]))}")
+            parts.append(f"{LABELS.get(b_, b_)}={int(np.median(st[:, b_] - st[:, a_]))}")
         tot = int(np.median(st[:, live[-1]] - st[:, live[0]]))
         print(f"s{s}l{l} total {tot}: " + " ".join(parts), flush=True)
