@@ -88,5 +88,7 @@ void pack_mk_weights(const float* w, int nout, int nin, std::vector<_Float16>& p
 void launch_mk_linear_test(const float* A, int K, const MkLin& W, int N, float* out, hipStream_t st);
 void launch_decoder_mk(const MkArgs& a, hipStream_t st);
 void launch_decoder_mk_init(const MkInitArgs& a, hipStream_t st);
+// read [p, p + bytes) once so the decoder weights are cache-resident (MALL) when the first launch streams them
+void launch_mk_prefetch(const void* p, size_t bytes, hipStream_t st);
 
 }  // namespace ddmi
