@@ -63,6 +63,8 @@ _SIGS = {
     "dd_op_last_error": (ctypes.c_char_p, []),
     "dd_op_last_kernel": (ctypes.c_char_p, []),
     "dd_op_mk_linear": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p, ctypes.c_int, c_void_p]),
+    "dd_op_bevproj": (ctypes.c_int, [c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p]),
     "dd_build_camera": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int,
                                        ctypes.c_int, c_void_p]),
     "dd_build_lidar": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int,

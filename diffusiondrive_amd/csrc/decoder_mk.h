@@ -91,4 +91,22 @@ void launch_decoder_mk_init(const MkInitArgs& a, hipStream_t st);
 // read [p, p + bytes) once so the decoder weights are cache-resident (MALL) when the first launch streams them
 void launch_mk_prefetch(const void* p, size_t bytes, hipStream_t st);
 
+// Fused bev_proj (bevproj.hip): out = LN(ReLU(bilinear(kvp) + W_p3 p3 + b)) per BEV pixel, W_p3 = the
+// p3 columns (256..319) of bev_proj.0 as an MkLin image (nks = 4)
+struct BevProjArgs {
+  const float* p3 = nullptr;  // [B*H*W] pixel rows of 64 channels at stride p3_ld floats
+  int64_t p3_ld = 0;
+  const float* kvp = nullptr;  // [B][Hk][Wk][256] = W[:, :256] keyval, no bias
+  const uint4* w = nullptr;
+  const float* s = nullptr;
+  const float* bias = nullptr;
+  const float* g = nullptr;  // LayerNorm
+  const float* beta = nullptr;
+  float* out = nullptr;  // [B*H*W][256]
+  int B = 0, H = 0, W = 0, Hk = 0, Wk = 0;
+  unsigned* flags = nullptr;
+};
+bool bevproj_supported(int C, int cin, int H, int W, int Hk, int Wk);
+void launch_bevproj(const BevProjArgs& a, hipStream_t st);
+
 }  // namespace ddmi

@@ -58,6 +58,40 @@ int dd_op_mk_linear(const float* A, int K, const float* wgt, const float* bias, 
   });
 }
 
+int dd_op_bevproj(const float* p3, int64_t p3_ld, const float* kvp, const float* wgt, const float* bias,
+                  const float* ln_g, const float* ln_b, float* out, int B, int H, int W, int Hk, int Wk, void* stream) {
+  return op_guard([&] {
+    if (!bevproj_supported(256, 64, H, W, Hk, Wk)) throw std::invalid_argument("dd_op_bevproj: unsupported shape");
+    std::vector<float> hw((size_t)256 * 64);
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));
+    DD_HIP_CHECK(hipMemcpy(hw.data(), wgt, hw.size() * sizeof(float), hipMemcpyDeviceToHost));
+    std::vector<_Float16> pk;
+    std::vector<float> sinv;
+    pack_mk_weights(hw.data(), 256, 64, pk, sinv);
+    Arena ar;
+    const size_t wo = ar.add(reinterpret_cast<const float*>(pk.data()), pk.size() / 2);
+    const size_t so = ar.add(sinv);
+    ar.upload();
+    BevProjArgs a;
+    a.p3 = p3;
+    a.p3_ld = p3_ld;
+    a.kvp = kvp;
+    a.w = reinterpret_cast<const uint4*>(ar.ptr(wo));
+    a.s = ar.ptr(so);
+    a.bias = bias;
+    a.g = ln_g;
+    a.beta = ln_b;
+    a.out = out;
+    a.B = B;
+    a.H = H;
+    a.W = W;
+    a.Hk = Hk;
+    a.Wk = Wk;
+    launch_bevproj(a, S(stream));
+    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));
+  });
+}
+
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias, const float* res,
                  float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {
   return op_guard([&] {

@@ -134,8 +134,10 @@ class Model {
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
   bool value_dedup = true;
-  // bev_proj's keyval half at 8 x 8 before the upsample (DDMI_BEVPROJ_LOWRES=0: concat at 64 x 64)
-  bool bevproj_lowres = true;
+  // bev_proj (DDMI_BEVPROJ): 2 "fused" = one bevproj.hip pass (f16x3 / bf16 modes; fp32 mode uses 1),
+  // 1 "lowres" = keyval half at 8 x 8, upsample, K = 64 GEMM, LayerNorm; 0 "concat" = concat at 64 x 64
+  int bevproj_mode = 2;
+  MkLinOff m_bevp3;  // bev_proj.0's p3 columns as a fragment-order f16x3 image (bevproj.hip)
   // f16x3 + gathered value rows: the trajectory head as one megakernel launch per (step, layer)
   // (decoder_mk.hip; DDMI_DECODER_MK=0: the unfused per-op chain)
   bool decoder_mk = true;
@@ -167,7 +169,12 @@ class Model {
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_BEVPROJ_LOWRES")) bevproj_lowres = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_BEVPROJ")) {
+      if (!strcmp(e, "fused")) bevproj_mode = 2;
+      else if (!strcmp(e, "lowres")) bevproj_mode = 1;
+      else if (!strcmp(e, "concat")) bevproj_mode = 0;
+      else throw std::invalid_argument(std::string("DDMI_BEVPROJ must be fused, lowres or concat, got ") + e);
+    }
     if (const char* e = getenv("DDMI_DECODER_MK")) decoder_mk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
@@ -372,6 +379,15 @@ class Model {
     }
     bevproj = prep_linear(bx, ar, "bev_proj.0", d, 320);
     bevproj_ln = prep_ln(bx, ar, "bev_proj.2", d);
+    if (bevproj_supported(d, 64, cfg.lidar_h / 4, cfg.lidar_w / 4, 8, 8)) {
+      Lin p3 = bevproj;  // the p3 columns 256..319 as a [256][64] Linear for the image
+      std::vector<float> w((size_t)d * 64);
+      for (int r = 0; r < d; ++r)
+        for (int k = 0; k < 64; ++k) w[(size_t)r * 64 + k] = ar.host(bevproj.w)[(size_t)r * 320 + 256 + k];
+      p3.w = ar.add(w);
+      p3.nin = 64;
+      m_bevp3 = pack_mk(p3);
+    }
     // decoder megakernel images (the reference configuration only)
     mk_ready = decoder_mk_supported(Q, P, d, 30, cfg.lidar_h / 4, cfg.lidar_w / 4, 1024);
     if (mk_ready) {
@@ -1081,13 +1097,33 @@ class Model {
 
     const int MB = B * HB * WB;
     float* cross = buf("cross_bev", (size_t)MB * d);
-    if (bevproj_lowres) {
+    const int bp_mode = (bevproj_mode == 2 && (gemm_mode == DD_GEMM_FP32 || m_bevp3.w == kNone)) ? 1 : bevproj_mode;
+    if (bp_mode >= 1) {
       // bev_proj(cat(bilinear(keyval 8x8), p3)) = bilinear(W[:, :256] keyval) + W[:, 256:] p3 + b: bilinear
       // interpolation is linear with weights summing to 1, so the keyval half of the 320 -> 256 projection runs
       // on the 8 x 8 tokens and is upsampled into cross_bev, which the p3 half (K = 64) then adds to in place
       float* kvp = buf("kv_proj", (size_t)B * 64 * d);
       gemm_slice(bevproj, 0, d, false, KV, (int64_t)65 * d, d, B, 64, kvp, (int64_t)64 * d, d, false, nullptr, 0, 0);
-      {
+      if (bp_mode == 2) {
+        // one pass: p3 in, cross_bev out (bevproj.hip)
+        BevProjArgs a;
+        a.p3 = cross_in + 256;
+        a.p3_ld = CC;
+        a.kvp = kvp;
+        a.w = reinterpret_cast<const uint4*>(W(m_bevp3.w));
+        a.s = W(m_bevp3.s);
+        a.bias = W(bevproj.b);
+        a.g = W(bevproj_ln.g);
+        a.beta = W(bevproj_ln.b);
+        a.out = cross;
+        a.B = B;
+        a.H = HB;
+        a.W = WB;
+        a.Hk = 8;
+        a.Wk = 8;
+        a.flags = num_flags;
+        launch("bevproj", 2.0 * MB * 64 * d * 3, [&] { launch_bevproj(a, st); });
+      } else {
         View4 a{kvp, (int64_t)64 * d, (int64_t)8 * d, d, 1};
         View4 o{cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, 1};
         launch("bilinear", 0, [&] { launch_bilinear(a, B, 8, 8, d, o, HB, WB, 8.0f / HB, 8.0f / WB, 0, st); });

@@ -150,6 +150,12 @@ const char* dd_op_last_kernel(void);
 /* The decoder megakernel's GEMM core (decoder_mk.hip): out[32][N] = A[32][K] W^T + bias, A and W fp32 (W
  * [N][K] packed on the host into the MFMA-fragment f16x3 image), K % 256 == 0, N % 32 == 0; synchronous. */
 int dd_op_mk_linear(const float* A, int K, const float* wgt, const float* bias, float* out, int N, void* stream);
+/* Fused bev_proj (transfuser_model_v2.py:123-140 concat_cross_bev + bev_proj): out[B*H*W][256] =
+ * LayerNorm(ReLU(bilinear(kvp [B][Hk][Wk][256]) + p3 wgt^T + bias)) with p3 rows of 64 channels at stride
+ * p3_ld floats and wgt [256][64] = bev_proj.0's p3 columns; kvp = bev_proj.0's keyval columns applied to
+ * the Hk x Wk keyval tokens. Synchronises the stream. */
+int dd_op_bevproj(const float* p3, int64_t p3_ld, const float* kvp, const float* wgt, const float* bias,
+                  const float* ln_g, const float* ln_b, float* out, int B, int H, int W, int Hk, int Wk, void* stream);
 /* NHWC conv: in (B,H,W,Cin), wgt (Cout,KH,KW,Cin), optional bias (Cout), res (B,Ho,Wo,Cout). */
 int dd_op_conv2d(const float* in, int B, int H, int W, int Cin, const float* wgt, const float* bias,
                  const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream);

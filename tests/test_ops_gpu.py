@@ -403,3 +403,25 @@ def test_mk_linear_core(gpu, K, N):
     ad, wd, bd = g(a), g(w), g(b)
     ok(gpu.dd_op_mk_linear(ad.data_ptr(), K, wd.data_ptr(), bd.data_ptr(), out.data_ptr(), N, None), gpu)
     close(out, ref, 3e-5)
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_bevproj_fused(gpu, B):
+    """bevproj.hip: LayerNorm(ReLU(bilinear(kvp 8x8 -> 64x64) + p3 W_p3^T + b)) in one pass vs PyTorch fp64
+    on the same decomposition (transfuser_model_v2.py:123-140 with the keyval half projected at 8 x 8);
+    p3 strided inside a 320-channel concat buffer as in the forward."""
+    H = W = 64
+    cat = rnd(B * H * W, 320, seed=101)
+    p3 = cat[:, 256:]
+    kvp = rnd(B, 8, 8, 256, seed=102)
+    w = rnd(256, 64, seed=103, scale=1.0 / 8.0)
+    bias = rnd(256, seed=104)
+    lg, lb = 1.0 + 0.1 * rnd(256, seed=105), rnd(256, seed=106)
+    bil = F.interpolate(kvp.double().permute(0, 3, 1, 2), size=(H, W), mode="bilinear", align_corners=False)
+    v = F.relu(p3.double() @ w.double().T + bias.double() + bil.permute(0, 2, 3, 1).reshape(-1, 256))
+    ref = F.layer_norm(v, (256,), lg.double(), lb.double(), 1e-5)
+    out = torch.empty(B * H * W, 256, device=DEV)
+    cd, kd, wd, bd, gd, ld = g(cat), g(kvp), g(w), g(bias), g(lg), g(lb)
+    ok(gpu.dd_op_bevproj(cd.data_ptr() + 256 * 4, 320, kd.data_ptr(), wd.data_ptr(), bd.data_ptr(), gd.data_ptr(),
+                         ld.data_ptr(), out.data_ptr(), B, H, W, 8, 8, None), gpu)
+    close(out, ref, 3e-5)
