@@ -58,7 +58,7 @@ KERNEL_DESC = {
     "conv_x6": "conv_x6 (halo-reuse direct 3x3 conv on v_mfma_f32_32x32x16_{f16 x3 | bf16})",
 }
 CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm")
-OTHER_KERNELS = ("stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample", "decoder", "bevproj", "misc")
+OTHER_KERNELS = ("stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample", "decoder", "tfdec", "bevproj", "misc")
 DTYPE = {
     "fp32": "fp32",
     "f16x3": "fp32 via f16x3 (each fp32 operand = hi+lo fp16, products ah*bh+ah*bl+al*bh, fp32 accumulate)",

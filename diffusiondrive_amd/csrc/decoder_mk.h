@@ -91,6 +91,31 @@ void launch_decoder_mk_init(const MkInitArgs& a, hipStream_t st);
 // read [p, p + bytes) once so the decoder weights are cache-resident (MALL) when the first launch streams them
 void launch_mk_prefetch(const void* p, size_t bytes, hipStream_t st);
 
+// Transformer-decoder megakernel (tfdec_mk.hip): V2TransfuserModel._tf_decoder (3 post-norm
+// nn.TransformerDecoderLayer, d 256, 8 heads, ffn 1024, ReLU; transfuser_model_v2.py:141-142) over the 31
+// queries of one scene per workgroup, then the trajectory head's step-invariant hoists of those queries: the
+// agent K / V projections and the ego attention (out_proj(v_proj(ego))) of both diffusion layers.
+struct TfMkLayer {
+  MkLin sa_in, sa_out, ca_q, ca_out, l1, l2;  // sa_in: 768 outputs (q | k | v); l1: 1024; l2: K = 1024
+  const float *n1g = nullptr, *n1b = nullptr, *n2g = nullptr, *n2b = nullptr, *n3g = nullptr, *n3b = nullptr;
+};
+struct TfMkArgs {
+  const TfMkLayer* layers = nullptr;  // [3] in device memory (read field by field; a by-value array in the
+                                      // kernel arguments ended up copied to registers / scratch)
+  const float* qemb = nullptr;  // [31][256] query embedding (the same for every scene)
+  const float* kvx = nullptr;   // [B][65][1536]: layer l's cross-attention K | V of the memory at columns l * 512
+  float* query_out = nullptr;   // [B][31][256]
+  MkLin ag_kv[2], eg_v[2], eg_out[2];
+  float* akv[2] = {nullptr, nullptr};  // [B][30][512]
+  float* ego[2] = {nullptr, nullptr};  // [B][256]
+  int B = 0;
+  unsigned* flags = nullptr;
+  unsigned long long* stamps = nullptr;  // diagnostics (stamps build): [B][40] shader-clock stamps per phase
+};
+bool tfdec_mk_supported(int nq, int nmem, int d, int heads, int ffn, int layers);
+bool tfdec_mk_layer_ok(const TfMkLayer& L);  // weight-image shapes of one layer (host check)
+void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st);
+
 // Fused bev_proj (bevproj.hip): out = LN(ReLU(bilinear(kvp) + W_p3 p3 + b)) per BEV pixel, W_p3 = the
 // p3 columns (256..319) of bev_proj.0 as an MkLin image (nks = 4)
 struct BevProjArgs {

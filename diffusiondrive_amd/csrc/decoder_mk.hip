@@ -31,6 +31,7 @@
 // A-operand buffers (together the K = 512 embedding operand, or the scene's agent K / V during the
 // attention), small per-query state. Weights stream from L2 straight into the MFMA operand registers.
 #include "decoder_mk.h"
+#include "mk_core.h"
 
 #include <algorithm>
 #include <cmath>
@@ -39,15 +40,8 @@ namespace ddmi {
 
 namespace {
 
-typedef _Float16 mk_h8 __attribute__((ext_vector_type(8)));
-typedef float mk_f16 __attribute__((ext_vector_type(16)));
-
 constexpr int kQ = 20, kP = 8, kD = 256, kA = 30, kNH = 8, kHD = 32, kHV = 64, kFF = 1024;
 constexpr int kQP = kQ * kP;
-constexpr int NT = 512;
-constexpr int FP = 260;   // fp32 row pitch (floats)
-constexpr int HP = 264;   // split row pitch (halfs), K = 256: 528 B, 16 mod 256 -> conflict-free b128 reads
-constexpr int HP2 = 520;  // split row pitch (halfs), K = 512: 1040 B
 constexpr int OFF_T1 = 32 * FP * 4;
 constexpr int OFF_SA = 2 * 32 * FP * 4;               // 66560
 constexpr int SPLIT_BYTES = 32 * HP * 2;              // one hi or lo image, K = 256
@@ -72,12 +66,6 @@ __device__ inline float norm_x(float x) { return 2.f * (x + 1.2f) / 56.9f - 1.f;
 __device__ inline float norm_y(float y) { return 2.f * (y + 20.f) / 46.f - 1.f; }
 __device__ inline float denorm_x(float x) { return (x + 1.f) / 2.f * 56.9f - 1.2f; }
 __device__ inline float denorm_y(float y) { return (y + 1.f) / 2.f * 46.f - 20.f; }
-
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 // F.grid_sample bilinear geometry (align_corners=False) of a trajectory point (blocks.py:101-122),
 // the arithmetic of decoder.hip's bev_tap_geometry
@@ -161,131 +149,6 @@ __device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int*
   }
 }
 
-// acc += A[32][aks*16 .. (aks+NKS)*16) (split LDS images, row pitch hp halfs) x W[:, wks*16 ..]^T for
-// the 32 output columns of tile nt: the NKS fragment pairs of the wave are loaded first (2 KB contiguous
-// per fragment per wave), then 3 f16 MFMAs per k16 step (small terms first, as conv_x3)
-// The B (weight) fragments stream through a ring of PF fragment pairs per wave (PF x 32 B per lane). A GEMM
-// starts with its first PF steps already in the ring and, as its last PF steps free their slots, loads the
-// first PF steps of the NEXT GEMM (`nx`, tile nnt, k-step nwks), so those loads fly under this GEMM's tail,
-// its epilogue, the barrier and whatever LDS / VALU phase separates the two GEMMs.
-constexpr int PF = 8;
-struct Ring {
-  uint4 h[PF], l[PF];
-};
-
-__device__ inline const uint4* mk_wbase(const MkLin& L, int nt, int wks) {
-  return L.w + ((size_t)(nt * L.nks + wks) * 64 + (threadIdx.x & 63)) * 2;
-}
-
-__device__ inline void ring_fill(Ring& R, const MkLin& L, int nt, int wks) {
-  const uint4* wb = mk_wbase(L, nt, wks);
-#pragma unroll
-  for (int s = 0; s < PF; ++s) {
-    R.h[s] = wb[s * 128];
-    R.l[s] = wb[s * 128 + 1];
-  }
-}
-
-// acc += A[32][aks*16 .. (aks+NKS)*16) (split LDS images, row pitch hp halfs) x W[:, wks*16 ..]^T for the 32
-// output columns of tile nt, 3 f16 MFMAs per k16 step (small terms first, as conv_x3); R holds this GEMM's
-// first PF steps on entry and the next GEMM's (nx) on exit (nx.w == nullptr: nothing next)
-template <int NKS>
-__device__ inline void mk_gemm(const char* ahi, const char* alo, int hp, const MkLin& L, int nt, int wks, mk_f16& acc,
-                               int aks, Ring& R, const MkLin& nx, int nnt, int nwks) {
-  static_assert(NKS % PF == 0 && NKS >= PF, "ring");
-  __builtin_amdgcn_sched_barrier(0);
-  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
-  const uint4* wb = mk_wbase(L, nt, wks);
-  const uint4* nb = nx.w ? mk_wbase(nx, nnt, nwks) : nullptr;
-  const int aoff = li * hp * 2 + hh * 16 + aks * 32;
-#pragma unroll
-  for (int s = 0; s < NKS; ++s) {
-    const mk_h8 ah = *reinterpret_cast<const mk_h8*>(ahi + aoff + s * 32);
-    const mk_h8 al = *reinterpret_cast<const mk_h8*>(alo + aoff + s * 32);
-    const mk_h8 wh = __builtin_bit_cast(mk_h8, R.h[s % PF]), wl = __builtin_bit_cast(mk_h8, R.l[s % PF]);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wh, acc, 0, 0, 0);
-    if (s + PF < NKS) {
-      R.h[s % PF] = wb[(s + PF) * 128];
-      R.l[s % PF] = wb[(s + PF) * 128 + 1];
-    } else if (nb) {
-      const int t = s + PF - NKS;
-      R.h[s % PF] = nb[t * 128];
-      R.l[s % PF] = nb[t * 128 + 1];
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-__device__ inline void zero_acc(mk_f16& acc) {
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-}
-
-// epilogue: f(row, col, acc * s + b) for this lane's 16 accumulator rows (C/D map of the 32x32 MFMA:
-// column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)); non-finite accumulators of live rows
-// (an activation beyond the fp16 range met the split) raise the numerics flag
-template <class F>
-__device__ inline void mk_epi(const mk_f16& acc, const MkLin& L, int nt, unsigned* flags, F&& f) {
-  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
-  const int col = nt * 32 + li;
-  const float s = L.s[col], bias = L.b ? L.b[col] : 0.f;
-  bool bad = false;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
-    if (row < kQ) bad |= !__builtin_isfinite(acc[r]);
-    f(row, col, acc[r] * s + bias);
-  }
-  if (bad && flags) atomicOr(flags, (unsigned)DD_NUM_F16_OVERFLOW);
-}
-
-__device__ inline void st_split(char* hi, int hp, int row, int col, float v) {
-  const _Float16 h = (_Float16)v;
-  const _Float16 l = (_Float16)(v - (float)h);
-  reinterpret_cast<_Float16*>(hi)[row * hp + col] = h;
-  reinterpret_cast<_Float16*>(hi + 32 * hp * 2)[row * hp + col] = l;
-}
-
-// 4 consecutive columns of a row into a split buffer (8 B hi, 8 B lo)
-__device__ inline void st_split4(char* hi, int hp, int row, int c4, float4 v) {
-  _Float16 h[4], l[4];
-  const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    h[e] = (_Float16)x[e];
-    l[e] = (_Float16)(x[e] - (float)h[e]);
-  }
-  uint2 hv, lv;
-  __builtin_memcpy(&hv, h, 8);
-  __builtin_memcpy(&lv, l, 8);
-  *reinterpret_cast<uint2*>(hi + (row * hp + c4) * 2) = hv;
-  *reinterpret_cast<uint2*>(hi + 32 * hp * 2 + (row * hp + c4) * 2) = lv;
-}
-
-// LayerNorm(256) of one row held as one float4 per lane (layernorm_v4's arithmetic, eps 1e-5)
-__device__ inline float4 ln256(float4 v, const float* g, const float* b, int lane) {
-  float s = (v.x + v.y) + (v.z + v.w);
-  s = wave_sum(s);
-  const float mean = s / 256.f;
-  const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
-  float q = (dx * dx + dy * dy) + (dz * dz + dw * dw);
-  q = wave_sum(q);
-  const float rstd = rsqrtf(q / 256.f + 1e-5f);
-  const float4 gg = reinterpret_cast<const float4*>(g)[lane], bb = reinterpret_cast<const float4*>(b)[lane];
-  float4 o;
-  o.x = (v.x - mean) * rstd * gg.x + bb.x;
-  o.y = (v.y - mean) * rstd * gg.y + bb.y;
-  o.z = (v.z - mean) * rstd * gg.z + bb.z;
-  o.w = (v.w - mean) * rstd * gg.w + bb.w;
-  return o;
-}
-
-__device__ inline float4 relu4(float4 v) {
-  return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-}
-
 __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* X1 = reinterpret_cast<float*>(lds);
@@ -349,7 +212,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     mk_f16 acc;
     zero_acc(acc);
     mk_gemm<32>(EH, EH + 32 * HP2 * 2, HP2, a.A.pa0, wave, 0, acc, 0, R, a.A.pa3, wave, 0);
-    mk_epi(acc, a.A.pa0, wave, a.flags, [&](int row, int col, float v) { T1[row * FP + col] = fmaxf(v, 0.f); });
+    mk_epi<kQ>(acc, a.A.pa0, wave, a.flags, [&](int row, int col, float v) { T1[row * FP + col] = fmaxf(v, 0.f); });
     __syncthreads();
     stamp(2);
 #pragma unroll
@@ -362,7 +225,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     stamp(3);
     zero_acc(acc);
     mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, a.A.pa3, wave, 0, acc, 0, R, L.outp, wave, 0);
-    mk_epi(acc, a.A.pa3, wave, a.flags, [&](int row, int col, float v) {
+    mk_epi<kQ>(acc, a.A.pa3, wave, a.flags, [&](int row, int col, float v) {
       if (row < kQ) {
         X1[row * FP + col] = v;
         a.tfe[(int64_t)(row0 + row) * kD + col] = v;
@@ -470,7 +333,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   mk_f16 acc;
   zero_acc(acc);
   mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.outp, wave, 0, acc, 0, R, L.ag_q, wave, 0);
-  mk_epi(acc, L.outp, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<kQ>(acc, L.outp, wave, a.flags, [&](int row, int col, float v) {
     float x = 0.f;
     if (row < kQ) {
       x = v + X1[row * FP + col];
@@ -484,7 +347,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // ================================================================ cross_agent_attention (+ norm1)
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ag_q, wave, 0, acc, 0, R, L.ag_out, wave, 0);
-  mk_epi(acc, L.ag_q, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<kQ>(acc, L.ag_q, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) T1[row * FP + col] = v;
   });
   // the scene's agent K | V rows into the two split buffers (free until the output is written; the
@@ -571,7 +434,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // out_proj + residual
   zero_acc(acc);
   mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ag_out, wave, 0, acc, 0, R, L.ffn0, wave, 0);
-  mk_epi(acc, L.ag_out, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<kQ>(acc, L.ag_out, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) X1[row * FP + col] = v + X1[row * FP + col];
   });
   __syncthreads();
@@ -600,7 +463,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   for (int c = 0; c < kFF / kD; ++c) {
     zero_acc(acc);
     mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ffn0, c * 8 + wave, 0, acc, 0, R, L.ffn2, wave, c * 16);
-    mk_epi(acc, L.ffn0, c * 8 + wave, a.flags,
+    mk_epi<kQ>(acc, L.ffn0, c * 8 + wave, a.flags,
            [&](int row, int col, float v) { st_split(SA, HP, row, col - c * kD, row < kQ ? fmaxf(v, 0.f) : 0.f); });
     __syncthreads();
     stamp(16 + 2 * c);
@@ -610,7 +473,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     __syncthreads();
     stamp(17 + 2 * c);
   }
-  mk_epi(acc2, L.ffn2, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<kQ>(acc2, L.ffn2, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) T1[row * FP + col] = v;
   });
   __syncthreads();
@@ -635,12 +498,12 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // ================================================================ task decoder: cls and reg branches
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c0, wave, 0, acc, 0, R, L.r0, wave, 0);
-  mk_epi(acc, L.c0, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<kQ>(acc, L.c0, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
   });
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.r0, wave, 0, acc, 0, R, L.c3, wave, 0);
-  mk_epi(acc, L.r0, wave, a.flags, [&](int row, int col, float v) { st_split(SA, HP, row, col, row < kQ ? fmaxf(v, 0.f) : 0.f); });
+  mk_epi<kQ>(acc, L.r0, wave, a.flags, [&](int row, int col, float v) { st_split(SA, HP, row, col, row < kQ ? fmaxf(v, 0.f) : 0.f); });
   __syncthreads();
   stamp(26);
 #pragma unroll
@@ -653,12 +516,12 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   stamp(27);
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c3, wave, 0, acc, 0, R, L.r2, wave, 0);
-  mk_epi(acc, L.c3, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<kQ>(acc, L.c3, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
   });
   zero_acc(acc);
   mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.r2, wave, 0, acc, 0, R, none, 0, 0);
-  mk_epi(acc, L.r2, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<kQ>(acc, L.r2, wave, a.flags, [&](int row, int col, float v) {
     if (row < kQ) X1[row * FP + col] = fmaxf(v, 0.f);
   });
   __syncthreads();
@@ -803,7 +666,7 @@ __global__ __launch_bounds__(NT, 1) void mk_linear_test_kernel(const float* __re
     ring_fill(R, W, nt, 0);
     for (int ks = 0; ks < K / 16; ks += 16)
       mk_gemm<16>(lds, lds + 32 * hp * 2, hp, W, nt, ks, acc, ks, R, ks + 16 < K / 16 ? W : none, nt, ks + 16);
-    mk_epi(acc, W, nt, nullptr, [&](int row, int col, float v) { out[row * N + col] = v; });
+    mk_epi<kQ>(acc, W, nt, nullptr, [&](int row, int col, float v) { out[row * N + col] = v; });
   }
 }
 

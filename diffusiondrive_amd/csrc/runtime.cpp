@@ -144,6 +144,16 @@ class Model {
   bool mk_ready = false;
   bool mk_stamps = false;  // diagnostics: per-phase clock stamps of the megakernel (tap "mk_stamps_s*l*")
   MkLinOff m_pa0, m_pa3;
+  // f16x3: the tf decoder + the trajectory head's agent / ego hoists as one megakernel launch (tfdec_mk.hip;
+  // DDMI_TFDEC_MK=0: the unfused per-op chain)
+  bool tfdec_mk = true;
+  bool tf_mk_ready = false;
+  struct TfMkW {
+    MkLinOff sa_in, sa_out, ca_q, ca_out, l1, l2;
+  } m_tf[3];
+  MkLinOff m_agkv[2], m_egv[2], m_egout[2];
+  Lin tf_cakv;  // the 3 layers' cross-attention K | V projections as one [1536][256] Linear
+  TfMkLayer* tf_mk_layers = nullptr;  // device copy of the 3 layers' megakernel parameters
   size_t dim_t_off = kNone;
   size_t mk_w_begin = 0, mk_w_end = 0;  // arena float range of the megakernel images (prefetched per forward)
   // graph cache keyed by the forward's shape signature and the buffer generation
@@ -161,6 +171,26 @@ class Model {
     build(bx);
     ar.upload();
     decoder_init_constants();
+    if (tf_mk_ready) {
+      TfMkLayer h[3];
+      for (int i = 0; i < 3; ++i) {
+        h[i].sa_in = mk(m_tf[i].sa_in);
+        h[i].sa_out = mk(m_tf[i].sa_out);
+        h[i].ca_q = mk(m_tf[i].ca_q);
+        h[i].ca_out = mk(m_tf[i].ca_out);
+        h[i].l1 = mk(m_tf[i].l1);
+        h[i].l2 = mk(m_tf[i].l2);
+        h[i].n1g = W(tf[i].n1.g);
+        h[i].n1b = W(tf[i].n1.b);
+        h[i].n2g = W(tf[i].n2.g);
+        h[i].n2b = W(tf[i].n2.b);
+        h[i].n3g = W(tf[i].n3.g);
+        h[i].n3b = W(tf[i].n3.b);
+        if (!tfdec_mk_layer_ok(h[i])) throw std::runtime_error("tfdec_mk: weight image shapes");
+      }
+      DD_HIP_CHECK(hipMalloc(&tf_mk_layers, sizeof(h)));
+      DD_HIP_CHECK(hipMemcpy(tf_mk_layers, h, sizeof(h), hipMemcpyHostToDevice));
+    }
     // default-priority streams: either one at the device's greatest priority measured 3-3.5 % slower
     // in the B = 64 bench graph, both at the least priority 33 % slower
     DD_HIP_CHECK(hipStreamCreateWithFlags(&st_main, hipStreamNonBlocking));
@@ -176,6 +206,7 @@ class Model {
       else throw std::invalid_argument(std::string("DDMI_BEVPROJ must be fused, lowres or concat, got ") + e);
     }
     if (const char* e = getenv("DDMI_DECODER_MK")) decoder_mk = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_TFDEC_MK")) tfdec_mk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
@@ -218,6 +249,7 @@ class Model {
     if (st_main) (void)hipStreamDestroy(st_main);
     if (st_side) (void)hipStreamDestroy(st_side);
     if (num_flags) (void)hipFree(num_flags);
+    if (tf_mk_layers) (void)hipFree(tf_mk_layers);
     for (auto& kv : bufs) (void)hipFree(kv.second.first);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& p : pending) {
@@ -387,6 +419,34 @@ class Model {
       p3.w = ar.add(w);
       p3.nin = 64;
       m_bevp3 = pack_mk(p3);
+    }
+    // tf-decoder megakernel images (tfdec_mk.hip)
+    tf_mk_ready = tfdec_mk_supported(31, 65, d, 8, 1024, (int)tf.size()) && dl.size() == 2;
+    if (tf_mk_ready) {
+      for (int i = 0; i < 3; ++i) {
+        m_tf[i].sa_in = pack_mk(tf[i].sa_in);
+        m_tf[i].sa_out = pack_mk(tf[i].sa_out);
+        m_tf[i].ca_q = pack_mk(tf[i].ca_q);
+        m_tf[i].ca_out = pack_mk(tf[i].ca_out);
+        m_tf[i].l1 = pack_mk(tf[i].l1);
+        m_tf[i].l2 = pack_mk(tf[i].l2);
+      }
+      for (int l = 0; l < 2; ++l) {
+        m_agkv[l] = pack_mk(dl[l].ag_kv);
+        m_egv[l] = pack_mk(dl[l].eg_v);
+        m_egout[l] = pack_mk(dl[l].eg_out);
+      }
+      std::vector<float> w, bsum;
+      for (int i = 0; i < 3; ++i) {
+        const Lin& c = tf[i].ca_kv;
+        w.insert(w.end(), ar.host(c.w), ar.host(c.w) + (size_t)c.nout * c.nin);
+        bsum.insert(bsum.end(), ar.host(c.b), ar.host(c.b) + c.nout);
+      }
+      tf_cakv.nout = 3 * 2 * d;
+      tf_cakv.nin = d;
+      tf_cakv.w = ar.add(w);
+      tf_cakv.x3 = prep_split(ar, w.data(), tf_cakv.nout, d);
+      tf_cakv.b = ar.add(bsum);
     }
     // decoder megakernel images (the reference configuration only)
     mk_ready = decoder_mk_supported(Q, P, d, 30, cfg.lidar_h / 4, cfg.lidar_w / 4, 1024);
@@ -1029,6 +1089,33 @@ class Model {
     float* akv[2];
     fork();
     side([&] {
+      if (tfdec_mk && tf_mk_layers && gemm_mode == DD_GEMM_F16X3) {
+        // the memory's cross-attention K | V of all 3 layers in one GEMM, then one megakernel launch
+        float* kvx = buf("tf_kvx", (size_t)B * 65 * 6 * d);
+        gemm(tf_cakv, KV, d, B * 65, kvx, 6 * d);
+        TfMkArgs t;
+        t.layers = tf_mk_layers;
+        for (int l = 0; l < 2; ++l) {
+          t.ag_kv[l] = mk(m_agkv[l]);
+          t.eg_v[l] = mk(m_egv[l]);
+          t.eg_out[l] = mk(m_egout[l]);
+          egos[l] = buf("ego_out" + std::to_string(l), (size_t)B * d);
+          akv[l] = buf("agent_kv" + std::to_string(l), (size_t)B * 30 * 2 * d);
+          t.akv[l] = akv[l];
+          t.ego[l] = egos[l];
+        }
+        t.qemb = W(q_emb);
+        t.kvx = kvx;
+        t.query_out = q;
+        t.B = B;
+        t.flags = num_flags;
+        if (mk_stamps) t.stamps = reinterpret_cast<unsigned long long*>(buf("tf_stamps", (size_t)B * 80));
+        // 2 x rows x sum(K x N): per layer q|k|v, 2 out_proj, cross q, FFN (+ the attention products), hoists
+        const double kn = 3.0 * (3584.0 * d) + 4.0 * d * d + 4.0 * d * d;
+        const double att = 3.0 * 8 * (31.0 * 31 + 31.0 * 65) * 32 * 2;
+        launch("tfdec", 2.0 * B * (NQ * kn + att), [&] { launch_tfdec_mk(t, st); });
+        return;
+      }
       launch("misc", 0, [&] { launch_broadcast_rows(W(q_emb), NQ, q, B * NQ, d, st); });
       float* qkv = buf("tf_qkv", (size_t)B * NQ * 3 * d);
       float* att = buf("tf_att", (size_t)B * NQ * d);

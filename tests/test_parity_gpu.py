@@ -331,3 +331,49 @@ def test_decoder_megakernel_matches_unfused_chain(gpu_model, seeded_sd, monkeypa
     lines.append(f"  trajectory waypoint L2 {l2:.3e}")
     _report(lines)
     assert l2 <= WAYPOINT_L2_TOL
+
+
+def test_tf_decoder_megakernel_matches_unfused_chain(gpu_model, seeded_sd, monkeypatch):
+    """The f16x3 _tf_decoder (3 post-norm layers) plus the trajectory head's agent K / V and ego-attention
+    hoists run as ONE megakernel launch (tfdec_mk.hip); DDMI_TFDEC_MK=0 keeps the unfused chain. Same
+    inputs: the decoded queries, the hoisted agent K / V and ego rows within the 1e-4 bar (relative to the
+    tensor's scale), the trajectory within the waypoint bar, and the megakernel proven dispatched."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 4
+    inp = synthetic_inputs(B, 37)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"])
+    sizes = {"query_out": B * 31 * 256, "agent_kv0": B * 30 * 512, "agent_kv1": B * 30 * 512, "ego_out0": B * 256,
+             "ego_out1": B * 256}
+    names = tuple(sizes)
+    gpu_model.set_gemm_mode("f16x3")
+    try:
+        gpu_model.set_profiling(True)
+        gpu_model.reset_stats()
+        res = gpu_model.forward(feats, noise=nz)
+        out = res["trajectory"].numpy()
+        st = gpu_model.kernel_stats("tfdec")
+        gpu_model.set_profiling(False)
+        got = {k: gpu_model.tap(k).cpu().numpy()[: sizes[k]] for k in names}
+    finally:
+        gpu_model.set_profiling(False)
+        gpu_model.set_gemm_mode("fp32")
+    assert st["launches"] == 1, st
+    monkeypatch.setenv("DDMI_TFDEC_MK", "0")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+    m.set_profiling(True)
+    ref_out = m.forward(feats, noise=nz)["trajectory"].numpy()
+    assert m.kernel_stats("tfdec")["launches"] == 0
+    m.set_profiling(False)
+    lines = ["== tf-decoder megakernel vs unfused chain (f16x3, B=4)"]
+    for k, v in got.items():
+        r = m.tap(k).cpu().numpy()[: sizes[k]]
+        assert r.shape == v.shape, (k, r.shape, v.shape)
+        err = float(np.abs(v - r).max())
+        lines.append(f"  {k:10s} max abs err {err:.3e} (max |ref| {np.abs(r).max():.3e})")
+        assert err <= MODE_TOL * max(1.0, float(np.abs(r).max())), (k, err)
+    l2 = waypoint_l2(out, ref_out)
+    lines.append(f"  trajectory waypoint L2 {l2:.3e}")
+    _report(lines)
+    assert l2 <= WAYPOINT_L2_TOL
