@@ -8,8 +8,8 @@
 // unfused chain (bilinear into cross_bev, the K = 64 GEMM with a residual read of it, an in-place
 // LayerNorm) moves ~4.25 KB per pixel.
 //
-// Persistent workgroups of 8 waves (one per CU) step over 32-pixel tiles:
-//  * XCD-aware tile order (each XCD walks a contiguous eighth of the map: its L2 keeps only those
+// Workgroups of 8 waves (LDS: one per CU) each step over a chunk of 8 consecutive 32-pixel tiles:
+//  * XCD-aware chunk order (each XCD walks a contiguous eighth of the map: its L2 keeps only those
 //    scenes' kvp maps); cross_bev written non-temporally (streamed once);
 //  * a 4-stage LDS ring filled by LDS-DMA (buffer_load ... lds, no VGPRs) 3 tiles ahead: the p3 tile
 //    (32 x 64 fp32 in 256-B rows whose 16-B slots are XOR-swizzled by row, so a 16-row ds_read_b128
@@ -81,6 +81,7 @@ __device__ inline void bl_idx(int dst, float ratio, int in_size, int& i0, int& i
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kOOB = 0x80000000u;  // buffer offsets >= num_records read as zero
 constexpr int NS = 4;                   // LDS stages (tiles in flight)
+constexpr int TPW = 8;                  // tiles per workgroup
 constexpr int A_BYTES = TP * CIN * 4;   // p3 tile, 256-B rows, 16-B slots XOR-swizzled by row
 constexpr int K_BYTES = 2 * KC * 1024;  // kvp footprint [row][column][256]
 constexpr int STAGE = A_BYTES + K_BYTES;
@@ -130,12 +131,15 @@ __global__ __launch_bounds__(NT) void bevproj_kernel(BevProjArgs a, int ntiles) 
   const float sc = a.s[col], bs = a.bias[col];
   bool bad = false;
 
-  // XCD-aware tile order: the workgroups of XCD x (blockIdx % 8, round-robin dispatch) walk the x-th
-  // contiguous eighth of the tiles, so each XCD's L2 holds the kvp maps of B / 8 scenes
-  const int xcd = blockIdx.x & 7, nper = gridDim.x >> 3, slot = blockIdx.x >> 3;
-  const int t_beg = (int)(((int64_t)ntiles * xcd) >> 3) + slot;
+  // XCD-aware tile order: the workgroups of XCD x (blockIdx % 8, round-robin dispatch) take consecutive
+  // TPW-tile chunks of the x-th contiguous eighth of the tiles, so each XCD's L2 holds the kvp maps of
+  // B / 8 scenes. Chunks rather than a persistent grid: when another kernel holds some CUs (the tf
+  // decoder beside this one), the hardware hands the remaining chunks to the free CUs.
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int t_beg = (int)(((int64_t)ntiles * xcd) >> 3) + slot * TPW;
   const int t_end = (int)(((int64_t)ntiles * (xcd + 1)) >> 3);
-  const int n = t_beg < t_end ? (t_end - t_beg + nper - 1) / nper : 0;
+  const int n = t_beg < t_end ? min(TPW, t_end - t_beg) : 0;
+  constexpr int nper = 1;
 
   // tile geometry: a tile lies in one BEV row y (W % 32 == 0) and reads kvp rows y0, y1 at columns
   // xs .. xs + KC - 1 (clamped)
@@ -275,14 +279,9 @@ void launch_bevproj(const BevProjArgs& a, hipStream_t st) {
       (int64_t)a.B * a.H * a.W >= (1ll << 31))
     throw std::runtime_error("launch_bevproj: needs 256 outputs, 64 p3 channels, W % 32 == 0, Wk <= 6 W / 32");
   const int ntiles = a.B * a.H * a.W / TP;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    DD_HIP_CHECK(hipGetDevice(&dev));
-    DD_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  // one per CU, a multiple of 8 (the XCD split)
-  const int grid = std::max(8, std::min(ncu, ntiles) & ~7);
+  // 8 x the chunks of the largest XCD eighth
+  const int per_xcd = (ntiles + 7) / 8;
+  const int grid = 8 * ((per_xcd + TPW - 1) / TPW);
   hipLaunchKernelGGL(bevproj_kernel, dim3(grid), dim3(NT), 0, st, a, ntiles);
   DD_HIP_CHECK(hipGetLastError());
 }

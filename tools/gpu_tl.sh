@@ -1,8 +1,7 @@
 #!/bin/bash
-# GPU box: gpu tests, then the per-launch breakdown (tools/launch_log.py). Stops at the first failure.
+# GPU box: one two-stream kernel trace of the default bench graph (read with tools/tail_view.py gpurun_out/tl).
 set -u
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -q -m gpu -x -rf --timeout 300 --timeout-method thread ${TESTS:-} > gpurun_out/tests.log 2>&1
-rc=$?; echo "[tests] rc=$rc"; tail -4 gpurun_out/tests.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python tools/launch_log.py --gemm f16x3 --out gpurun_out/ll.md > gpurun_out/ll.log 2>&1
-rc=$?; echo "[ll] rc=$rc"; head -1 gpurun_out/ll.md; grep -A30 "GEMM / conv total" gpurun_out/ll.md; exit $rc
+R=${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p "$R/gpurun_out"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d "$R/gpurun_out/tl" -o run -- python "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-compare > "$R/gpurun_out/tl.log" 2>&1
+rc=$?; echo "[trace] rc=$rc"; grep '^{' "$R/gpurun_out/tl.log" | cut -c1-150; exit $rc
