@@ -98,7 +98,7 @@ _SIGS = {
     "dd_op_mha_small": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p]),
     "dd_op_gpt_attention": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                           ctypes.c_int, c_void_p]),
+                                           ctypes.c_int, ctypes.c_int, c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

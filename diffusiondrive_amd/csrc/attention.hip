@@ -20,9 +20,11 @@
 // Bound: fp32 MFMA (2 * 2 T^2 hs FLOP per (scene, head)); operands stay in L2 (qkv of one scene
 // 0.3-2.4 MB).
 #include <cmath>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
+#include "mk_core.h"
 
 namespace ddmi {
 
@@ -207,11 +209,315 @@ __global__ __launch_bounds__(256) void gpt_attn_kernel(const float* __restrict__
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// f16x3 form (the f16x3 / bf16 modes): NW waves per workgroup, one per 32-query block (T / 32 NW
+// workgroups per (scene, head); NW = 5 at T = 320 keeps <= 256 VGPRs per wave), flash-style over 32-key
+// tiles staged in LDS already split (K three ways as key rows, V two ways transposed to dimension rows;
+// double-buffered at hs <= 32, single at 64 / 128 so 2-3 workgroups share a CU), so no wave splits an
+// operand element more than once:
+//  * S^T = K Q^T on v_mfma_f32_32x32x16_f16 with both operands split three ways (6 products: the
+//    softmax turns score error into relative probability error) - keys on the accumulator rows,
+//    queries on the lanes, so each lane owns one query's online-softmax state (with lane ^ 32);
+//  * O = P V with P taken straight from the S^T accumulators as the A operand: an MFMA step's k order
+//    is free, so it is the C layout's key order (lane half hh, element e <-> key 16 s + 4 hh + (e & 3)
+//    + 8 (e >> 2)), and V's B fragment gathers the same keys from the staged rows;
+//    P and V split two ways (f16x3, as every other contraction of the path); O's C layout (lane = dimension, rows = queries) makes the final stores 128-B row segments; the
+//    per-query rescale / 1/l reach it through a 32-float LDS slot per wave.
+struct Split3 {
+  mk_h8 h, m, l;
+};
+__device__ inline Split3 split3(const float a[8]) {
+  Split3 s;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s.h[e] = (_Float16)a[e];
+    const float r = a[e] - (float)s.h[e];
+    s.m[e] = (_Float16)r;
+    s.l[e] = (_Float16)(r - (float)s.m[e]);
+  }
+  return s;
+}
+__device__ inline void mfma6s(mk_f16& acc, const Split3& a, const Split3& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.l, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.m, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.h, b.l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.m, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.h, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.h, b.h, acc, 0, 0, 0);
+}
+
+typedef _Float16 at_h2 __attribute__((ext_vector_type(2)));
+typedef float at_f2 __attribute__((ext_vector_type(2)));
+// pairs through v_cvt_pk_f16_f32: hi = f16(x), lo = f16(x - hi) [, lo2 = f16(x - hi - lo)]
+__device__ inline void split2x2(float a, float b, at_h2& hi, at_h2& lo) {
+  hi = __builtin_convertvector((at_f2){a, b}, at_h2);
+  const at_f2 f = __builtin_convertvector(hi, at_f2);
+  lo = __builtin_convertvector((at_f2){a - f.x, b - f.y}, at_h2);
+}
+__device__ inline void split3x2(float a, float b, at_h2& hi, at_h2& mi, at_h2& lo) {
+  hi = __builtin_convertvector((at_f2){a, b}, at_h2);
+  const at_f2 f = __builtin_convertvector(hi, at_f2);
+  const at_f2 r = (at_f2){a - f.x, b - f.y};
+  mi = __builtin_convertvector(r, at_h2);
+  const at_f2 g = __builtin_convertvector(mi, at_f2);
+  lo = __builtin_convertvector((at_f2){r.x - g.x, r.y - g.y}, at_h2);
+}
+
+// LDS images per stage of 32 keys (halfs): K split three ways [3][32 keys][HS + 8] (16-B rows 4 banks apart),
+// V^T split two ways [2][HS dims][36] (8-B reads of 4 consecutive keys, 18-dword rows -> conflict-free)
+template <int HS>
+struct AttnLds {
+  static constexpr int KPH = HS + 8;               // K image row pitch (halfs)
+  static constexpr int VPH = 36;                   // V^T image row pitch (halfs)
+  static constexpr int KIMG = 32 * KPH;            // halfs per K image
+  static constexpr int VIMG = HS * VPH;            // halfs per V^T image
+  static constexpr int STAGE = 3 * KIMG + 2 * VIMG;  // halfs per stage
+};
+
+template <int HS, int NW>
+__global__ __launch_bounds__(64 * NW) void gpt_attn_x3_kernel(const float* __restrict__ qkv, float* __restrict__ y, int T,
+                                                              int C, int heads, float scale) {
+  using LY = AttnLds<HS>;
+  constexpr int NB = HS >= 64 ? 1 : 2;  // LDS stages (one for the large heads: 2-3 workgroups per CU)
+  constexpr int NKS = HS / 16;           // k16 steps of the score product
+  constexpr int NDT = (HS + 31) / 32;    // 32-wide dimension tiles of O
+  constexpr int NT = 64 * NW;
+  constexpr int NKE = 32 * HS / 4;       // K float4 per tile
+  constexpr int NVE = 8 * HS;            // V (4 keys, 1 dim) groups per tile
+  constexpr int NPK = (NKE + NT - 1) / NT, NPV = (NVE + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) _Float16 LH[];
+  float* AL = reinterpret_cast<float*>(LH + NB * LY::STAGE) + (threadIdx.x >> 6) * 32;  // per-wave 32 floats
+  const int G = T / (32 * NW);  // workgroups per (scene, head)
+  const int bh = blockIdx.x / G, grp = blockIdx.x - bh * G;
+  const int b = bh / heads, h = bh - (bh / heads) * heads;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, hh = lane >> 5;
+  const int ld = 3 * C;
+  const float* base = qkv + (int64_t)b * T * ld;
+  const float* Qg = base + h * HS;
+  const float* Kg = base + C + h * HS;
+  const float* Vg = base + 2 * C + h * HS;
+  const int q0 = (grp * NW + wave) * 32;
+
+  Split3 qf[NKS];  // Q^T B fragments: k = head dimension, n = query q0 + li
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    float q8[8];
+    ld8(Qg + (int64_t)(q0 + li) * ld + 16 * ks + 8 * hh, q8);
+    qf[ks] = split3(q8);
+  }
+  // staging: K float4 e -> (row e / (HS/4), quad e % (HS/4)); V group e -> (dim e % HS, keys 4 (e / HS) ..)
+  float4 kr[NPK], vr[NPV];
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NPK; ++i) {
+      const int e = tid + NT * i;
+      if (e < NKE) {
+        const int row = e / (HS / 4), c4 = e - row * (HS / 4);
+        kr[i] = *reinterpret_cast<const float4*>(Kg + (int64_t)(32 * t + row) * ld + c4 * 4);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int e = tid + NT * i;
+      if (e < NVE) {
+        const int d = e % HS, k4 = e / HS;
+        const float* p = Vg + (int64_t)(32 * t + 4 * k4) * ld + d;
+        vr[i] = make_float4(p[0], p[ld], p[2 * ld], p[3 * ld]);
+      }
+    }
+  };
+  auto stage = [&](int buf) {
+    _Float16* S0 = LH + buf * LY::STAGE;
+#pragma unroll
+    for (int i = 0; i < NPK; ++i) {
+      const int e = tid + NT * i;
+      if (e < NKE) {
+        const int row = e / (HS / 4), c4 = e - row * (HS / 4);
+        at_h2 hv[2], mv[2], lv[2];
+        split3x2(kr[i].x, kr[i].y, hv[0], mv[0], lv[0]);
+        split3x2(kr[i].z, kr[i].w, hv[1], mv[1], lv[1]);
+        const int o = row * LY::KPH + c4 * 4;
+        uint2 u;
+        __builtin_memcpy(&u, hv, 8);
+        *reinterpret_cast<uint2*>(S0 + o) = u;
+        __builtin_memcpy(&u, mv, 8);
+        *reinterpret_cast<uint2*>(S0 + LY::KIMG + o) = u;
+        __builtin_memcpy(&u, lv, 8);
+        *reinterpret_cast<uint2*>(S0 + 2 * LY::KIMG + o) = u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int e = tid + NT * i;
+      if (e < NVE) {
+        const int d = e % HS, k4 = e / HS;
+        at_h2 hv[2], lv[2];
+        split2x2(vr[i].x, vr[i].y, hv[0], lv[0]);
+        split2x2(vr[i].z, vr[i].w, hv[1], lv[1]);
+        const int o = 3 * LY::KIMG + d * LY::VPH + 4 * k4;
+        uint2 u;
+        __builtin_memcpy(&u, hv, 8);
+        *reinterpret_cast<uint2*>(S0 + o) = u;
+        __builtin_memcpy(&u, lv, 8);
+        *reinterpret_cast<uint2*>(S0 + LY::VIMG + o) = u;
+      }
+    }
+  };
+
+  float m_run = -INFINITY, l_run = 0.f;
+  mk_f16 o[NDT];
+#pragma unroll
+  for (int d = 0; d < NDT; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  const int nt = T / 32;
+  fetch(0);
+  stage(0);
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) fetch(t + 1);
+    const _Float16* K0 = LH + (NB == 2 ? (t & 1) : 0) * LY::STAGE;
+    const _Float16* V0 = K0 + 3 * LY::KIMG;
+    // S^T = K Q^T, six products on pre-split images
+    mk_f16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int o = li * LY::KPH + 16 * ks + 8 * hh;
+      Split3 kf;
+      kf.h = *reinterpret_cast<const mk_h8*>(K0 + o);
+      kf.m = *reinterpret_cast<const mk_h8*>(K0 + LY::KIMG + o);
+      kf.l = *reinterpret_cast<const mk_h8*>(K0 + 2 * LY::KIMG + o);
+      mfma6s(s, kf, qf[ks]);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] *= scale;
+      mt = fmaxf(mt, s[r]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = __expf(m_run - m_new);  // 0 on the first tile (v_exp_f32 path: ~2 ulp)
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = __expf(s[r] - m_new);
+      ls += s[r];
+    }
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+    if (hh == 0) AL[li] = alpha;
+    // (one wave's LDS accesses complete in order: the reads below see this wave's writes); skipped when no
+    // query's running max moved (alpha == 1 in every lane), the common case after the first tiles
+    if (__any(alpha != 1.f))
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 a4 = *reinterpret_cast<const float4*>(AL + 8 * i + 4 * hh);  // queries 8i + 4hh + 0..3
+#pragma unroll
+      for (int d = 0; d < NDT; ++d) {
+        o[d][4 * i] *= a4.x;
+        o[d][4 * i + 1] *= a4.y;
+        o[d][4 * i + 2] *= a4.z;
+        o[d][4 * i + 3] *= a4.w;
+      }
+    }
+    // O += P V: P (A) from the accumulators and V (B), both split two ways: f16x3
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      mk_h8 ph, pl;  // P split two ways (hi, lo)
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        at_h2 a, c;
+        split2x2(s[8 * s2 + e], s[8 * s2 + e + 1], a, c);
+        ph[e] = a.x;
+        ph[e + 1] = a.y;
+        pl[e] = c.x;
+        pl[e + 1] = c.y;
+      }
+      const int kb = 16 * s2 + 4 * hh;  // keys kb .. kb+3 and kb+8 .. kb+11
+#pragma unroll
+      for (int d = 0; d < NDT; ++d) {
+        const int dim = 32 * d + li;
+        mk_h8 vh, vl;
+        if (HS % 32 == 0 || dim < HS) {
+          const _Float16* vp = V0 + dim * LY::VPH + kb;
+          const uint2 a0 = *reinterpret_cast<const uint2*>(vp), a1 = *reinterpret_cast<const uint2*>(vp + 8);
+          const uint2 b0 = *reinterpret_cast<const uint2*>(vp + LY::VIMG), b1 = *reinterpret_cast<const uint2*>(vp + LY::VIMG + 8);
+          vh = __builtin_bit_cast(mk_h8, make_uint4(a0.x, a0.y, a1.x, a1.y));
+          vl = __builtin_bit_cast(mk_h8, make_uint4(b0.x, b0.y, b1.x, b1.y));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vh[e] = vl[e] = (_Float16)0.f;
+        }
+        o[d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pl, vh, o[d], 0, 0, 0);
+        o[d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ph, vl, o[d], 0, 0, 0);
+        o[d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ph, vh, o[d], 0, 0, 0);
+      }
+    }
+    if (t + 1 < nt) {
+      if constexpr (NB == 1) __syncthreads();  // every wave is done with the stage before it is refilled
+      stage(NB == 2 ? (t + 1) & 1 : 0);
+    }
+    __syncthreads();
+  }
+  if (hh == 0) AL[li] = 1.f / l_run;
+  float* yb = y + ((int64_t)b * T + q0) * C + h * HS;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 inv = *reinterpret_cast<const float4*>(AL + 8 * i + 4 * hh);
+    const float iv[4] = {inv.x, inv.y, inv.z, inv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 8 * i + 4 * hh + j;
+#pragma unroll
+      for (int d = 0; d < NDT; ++d) {
+        const int dim = 32 * d + li;
+        if (HS % 32 == 0 || dim < HS) yb[(int64_t)row * C + dim] = o[d][4 * i + j] * iv[j];
+      }
+    }
+  }
+}
+
 }  // namespace
 
-void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, float* y, hipStream_t st) {
+void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, float* y, int prec, hipStream_t st) {
   if (heads <= 0 || C % heads) throw std::runtime_error("gpt_attention: C % heads != 0");
   const int hs = C / heads;
+  if (prec != 0) {
+    // f16x3 form: T % 32 == 0, NW (waves per workgroup) = the largest divisor of T / 32 that is <= 5
+    if (T % 32 || T > 1024 || (reinterpret_cast<uintptr_t>(qkv) & 15) || C % 4)
+      throw std::runtime_error("gpt_attention(f16x3): T % 32 == 0, T <= 1024, 16-B aligned qkv, C % 4 == 0");
+    const int nq = T / 32;
+    int nw = 5;
+    while (nq % nw) --nw;
+    const float scale = (float)(1.0 / std::sqrt((double)hs));
+    const dim3 grid((unsigned)((int64_t)B * heads * (nq / nw))), block((unsigned)(64 * nw));
+    const size_t lds = (size_t)(hs >= 64 ? 1 : 2) * (3 * 32 * (hs + 8) + 2 * hs * 36) * 2 + (size_t)nw * 32 * sizeof(float);
+    auto go = [&](auto HSC) {
+      constexpr int HS = decltype(HSC)::value;
+      switch (nw) {
+        case 5: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 5>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+        case 4: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 4>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+        case 3: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 3>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+        case 2: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 2>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+        default: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 1>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+      }
+    };
+    switch (hs) {
+      case 16: go(std::integral_constant<int, 16>()); break;
+      case 32: go(std::integral_constant<int, 32>()); break;
+      case 64: go(std::integral_constant<int, 64>()); break;
+      case 128: go(std::integral_constant<int, 128>()); break;
+      default:
+        throw std::runtime_error("gpt_attention(f16x3): head size " + std::to_string(hs) + " not in {16..128}");
+    }
+    DD_HIP_CHECK(hipGetLastError());
+    return;
+  }
   // phase 3 splits the keys into 4 contiguous lane-group slices read as 16-B LDS vectors
   if (T % 64 || (T / 4) % 8 || T > 512 || (T / 4) % 4)
     throw std::runtime_error("gpt_attention: T must be a multiple of 64 with T/4 % 8 == 0, and <= 512");

@@ -105,7 +105,8 @@ void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldr
 // Fused GPT self-attention (attention.hip): y[b,t,h*hs..] = softmax(q.k^T / sqrt(hs)) v per
 // (scene, head) from the packed projection qkv [B][T][3C]; y is [B][T][C]. T % 64 == 0, (T/4) % 8 == 0,
 // T <= 512, hs in {16, ..., 512}.
-void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, float* y, hipStream_t st);
+// prec 0: fp32 MFMA; 1: f16x3 MFMA (three-way split scores), the f16x3 / bf16 modes
+void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, float* y, int prec, hipStream_t st);
 // Row softmax of (scale * x), in place, rows of length L (<= 1024), row stride ld.
 void launch_softmax_rows(float* x, int64_t ld, int rows, int L, float scale, hipStream_t st);
 // dst[r][:] = src[r % nsrc][:] for r < rows (row length C, contiguous).

@@ -337,8 +337,8 @@ int dd_op_mha_small(const float* q, const float* k, const float* v, float* out, 
   });
 }
 
-int dd_op_gpt_attention(const float* qkv, float* y, int B, int T, int C, int heads, void* stream) {
-  return op_guard([&] { launch_gpt_attention(qkv, B, T, C, heads, y, S(stream)); });
+int dd_op_gpt_attention(const float* qkv, float* y, int B, int T, int C, int heads, int prec, void* stream) {
+  return op_guard([&] { launch_gpt_attention(qkv, B, T, C, heads, y, prec, S(stream)); });
 }
 
 }  // extern "C"

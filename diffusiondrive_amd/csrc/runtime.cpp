@@ -147,6 +147,7 @@ class Model {
   // f16x3: the tf decoder + the trajectory head's agent / ego hoists as one megakernel launch (tfdec_mk.hip;
   // DDMI_TFDEC_MK=0: the unfused per-op chain)
   bool tfdec_mk = true;
+  bool gpt_attn_x3 = true;  // f16x3 GPT attention in the f16x3 / bf16 modes (DDMI_GPT_ATTN_X3=0: the fp32-MFMA kernel)
   bool tf_mk_ready = false;
   struct TfMkW {
     MkLinOff sa_in, sa_out, ca_q, ca_out, l1, l2;
@@ -207,6 +208,7 @@ class Model {
     }
     if (const char* e = getenv("DDMI_DECODER_MK")) decoder_mk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_TFDEC_MK")) tfdec_mk = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_GPT_ATTN_X3")) gpt_attn_x3 = atoi(e) != 0;
     if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
@@ -974,8 +976,10 @@ class Model {
     for (const GptBlockW& w : g.blocks) {
       ln(w.ln1, X, C, Hb, C, M);
       gemm(w.qkv, Hb, C, M, QKV, 3 * C);
-      // softmax(Q K^T / sqrt(hs)) V per (scene, head), one fused fp32-MFMA launch (attention.hip)
-      launch("attn", 4.0 * B * T * T * (double)C, [&] { launch_gpt_attention(QKV, B, T, C, 4, Y, st); });
+      // softmax(Q K^T / sqrt(hs)) V per (scene, head), one fused launch (attention.hip): fp32 MFMA in the
+      // fp32 mode, f16x3 MFMA (three-way split scores) in the f16x3 / bf16 modes
+      const int aprec = (gemm_mode == DD_GEMM_FP32 || !gpt_attn_x3 || C / 4 > 128 || T % 32 || T > 1024) ? 0 : 1;
+      launch("attn", 4.0 * B * T * T * (double)C, [&] { launch_gpt_attention(QKV, B, T, C, 4, Y, aprec, st); });
       gemm(w.proj, Y, C, M, X, C, false, X, C);  // x = x + proj(y)
       ln(w.ln2, X, C, Hb, C, M);
       gemm(w.mlp0, Hb, C, M, MLP, 4 * C, true);

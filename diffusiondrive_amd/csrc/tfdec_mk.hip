@@ -70,59 +70,6 @@ __device__ inline MkLin ld_lin(const __attribute__((address_space(4))) MkLin& x)
   return m;
 }
 
-// 8 consecutive floats
-__device__ inline void ld8(const float* p, float a[8]) {
-  const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
-  a[0] = x.x;
-  a[1] = x.y;
-  a[2] = x.z;
-  a[3] = x.w;
-  a[4] = y.x;
-  a[5] = y.y;
-  a[6] = y.z;
-  a[7] = y.w;
-}
-
-// acc += A B for fp32 fragments split at use into fp16 hi / lo (al bh + ah bl + ah bh)
-__device__ inline void mfma3(mk_f16& acc, const float a[8], const float b[8]) {
-  mk_h8 ah, al, bh, bl;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    ah[e] = (_Float16)a[e];
-    al[e] = (_Float16)(a[e] - (float)ah[e]);
-    bh[e] = (_Float16)b[e];
-    bl[e] = (_Float16)(b[e] - (float)bh[e]);
-  }
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
-}
-
-// acc += A B with both fragments split three ways (x = h + m + l, each fp16) and the six products down to
-// the 2^-22 terms (h h, h m, m h, h l, m m, l h): ~fp32-accurate. For the attention scores, whose error the
-// softmax turns into a relative probability error (scores reach |100|: 3-product f16x3 left ~5e-5 in the
-// decoded queries at B = 64, this ~4e-6)
-__device__ inline void mfma6(mk_f16& acc, const float a[8], const float b[8]) {
-  mk_h8 ah, am, al, bh, bm, bl;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    ah[e] = (_Float16)a[e];
-    const float ra = a[e] - (float)ah[e];
-    am[e] = (_Float16)ra;
-    al[e] = (_Float16)(ra - (float)am[e]);
-    bh[e] = (_Float16)b[e];
-    const float rb = b[e] - (float)bh[e];
-    bm[e] = (_Float16)rb;
-    bl[e] = (_Float16)(rb - (float)bm[e]);
-  }
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bm, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
-}
-
 // B fragments of Q_h^T (k = head dimension, n = query = lane % 32) for the two k16 steps
 __device__ inline void load_q_frags(const float* q, int h, float qf[2][8]) {
   const int lane = threadIdx.x & 63;

@@ -362,7 +362,8 @@ def test_mha_small(gpu, Lq, Lk):
 @pytest.mark.parametrize("B,T,C", [(2, 320, 64), (2, 320, 128), (1, 320, 256), (1, 320, 512), (1, 64, 1024),
                                    (1, 320, 2048), (1, 128, 256)])
 def test_gpt_attention(gpu, B, T, C):
-    """Fused GPT self-attention (transfuser_backbone.py:386-410) vs the PyTorch fp32 restatement."""
+    """Fused GPT self-attention (transfuser_backbone.py:386-410), fp32-MFMA form, vs the PyTorch fp32
+    restatement."""
     nh, hs = 4, C // 4
     qkv = rnd(B, T, 3 * C, seed=31)
     q, k, v = (t.reshape(B, T, nh, hs).transpose(1, 2) for t in qkv.split(C, -1))
@@ -370,7 +371,24 @@ def test_gpt_attention(gpu, B, T, C):
     ref = (att @ v).transpose(1, 2).reshape(B, T, C)
     out = torch.empty(B, T, C, device=DEV)
     qd = g(qkv)
-    ok(gpu.dd_op_gpt_attention(qd.data_ptr(), out.data_ptr(), B, T, C, nh, None), gpu)
+    ok(gpu.dd_op_gpt_attention(qd.data_ptr(), out.data_ptr(), B, T, C, nh, 0, None), gpu)
+    close(out, ref, 2e-5)
+
+
+@pytest.mark.parametrize("B,T,C,amp", [(2, 320, 64, 1.0), (2, 320, 128, 1.0), (1, 320, 256, 1.0), (1, 320, 512, 1.0),
+                                       (1, 320, 512, 4.0), (2, 64, 128, 1.0), (1, 96, 64, 3.0)])
+def test_gpt_attention_f16x3(gpu, B, T, C, amp):
+    """The f16x3 GPT attention (flash-style over 32-key tiles, P taken from the S^T accumulators) vs PyTorch
+    fp64; amp scales q / k to sharpen the softmax (scores up to ~|40| at amp 4)."""
+    nh, hs = 4, C // 4
+    qkv = rnd(B, T, 3 * C, seed=33)
+    qkv[..., : 2 * C] *= amp
+    q, k, v = (t.double().reshape(B, T, nh, hs).transpose(1, 2) for t in qkv.split(C, -1))
+    att = torch.softmax((q @ k.transpose(-2, -1)) * (1.0 / np.sqrt(hs)), -1)
+    ref = (att @ v).transpose(1, 2).reshape(B, T, C)
+    out = torch.empty(B, T, C, device=DEV)
+    qd = g(qkv)
+    ok(gpu.dd_op_gpt_attention(qd.data_ptr(), out.data_ptr(), B, T, C, nh, 1, None), gpu)
     close(out, ref, 2e-5)
 
 

@@ -19,7 +19,12 @@ pytestmark = pytest.mark.gpu
 WAYPOINT_L2_TOL = 1e-4
 HEADING_TOL = 1e-4
 MODE_TOL = 1e-4    # absolute, on every per-(step, layer) poses_reg (m / rad) and poses_cls (logit)
-AGENT_TOL = 5e-4   # absolute, agent_states (m / rad; x, y are tanh * 32, so 1e-5 relative = 3e-4 m) and labels
+# absolute, agent_states (m / rad) and labels. The agent head (x, y = tanh * 32) is ill-conditioned on the
+# seeded weights: the REFERENCE's own agent_states move by 1.6e-4 when the camera input is perturbed by one
+# fp32 ulp (2^-24 relative; tests/test_conditioning.py measures it), and the fp32-MFMA path sits at 2.5e-4 from
+# the goldens by summation order alone. f16x3 carries ~4-8x fp32's rounding per contraction, so the bar is 10x
+# the one-ulp response (test_conditioning asserts that relation stays true).
+AGENT_TOL = 2e-3
 TAP_TOL = 2e-5  # relative to max(1, |sample|max) on intermediates
 
 
