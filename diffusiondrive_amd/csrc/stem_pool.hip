@@ -5,13 +5,13 @@
 // The unfused path writes the 64-channel stem map (1.07 GB at B = 64 for the camera) and reads it
 // back for the pool; here a workgroup owns a PH x PW tile of POOLED outputs, computes the
 // (2PH+1) x (2PW+1) stem pixels under it (the pool windows overlap by one stem row / column, which
-// is recomputed: 16 %), keeps them in LDS and writes only the pooled map.
+// is recomputed: 14 %), keeps them in LDS and writes only the pooled map.
 //
 // Arithmetic: f16x3 as conv_x3.hip (fp32 operands split into fp16 hi + lo, products al*bh + ah*bl +
 // ah*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation, per-channel power-of-two weight scale undone
 // in the epilogue, non-finite accumulators raise DD_NUM_F16_OVERFLOW), or (PREC 1, the bf16 mode) one
 // bf16 product per MAC on v_mfma_f32_32x32x16_bf16 from the bf16 weight image.
-//  * GEMM view per tile: M = stem pixels (297 -> 10 tiles of 32), N = 64 channels (2 tiles),
+//  * GEMM view per tile: M = stem pixels (255 -> 8 tiles of 32), N = 64 channels (2 tiles),
 //    K = 7 kh x 8 kw x 4 ch = 224 (kw = 7 is a zero tap): 14 k16 steps, each = one kernel row kh and
 //    four consecutive taps = 4 consecutive input pixels of that row.
 //  * A: the (4PH+7) x (4PW+8) input patch is split once into fp16 hi / lo images in LDS (8 B per
@@ -26,7 +26,7 @@
 //    one 16-B store per pooled pixel quad.
 //  * Persistent grid (one 8-wave workgroup per CU, ~111 KB LDS); the next tile's input patch is
 //    loaded into registers while the current tile's MFMAs run.
-// Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.16 x recompute,
+// Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.14 x recompute,
 // 224 / 196 K padding; HBM traffic = the input once (+ halo re-reads) + the pooled map.
 #include "common.h"
 
@@ -41,15 +41,20 @@ typedef float sp_f16 __attribute__((ext_vector_type(16)));
 typedef __bf16 sp_b8 __attribute__((ext_vector_type(8)));
 typedef __bf16 sp_b4 __attribute__((ext_vector_type(4)));
 
-constexpr int PH = 4, PW = 16;                     // pooled outputs per tile
-constexpr int SH = 2 * PH + 1, SW = 2 * PW + 1;    // stem pixels per tile (9 x 33)
-constexpr int NSP = SH * SW;                       // 297
-constexpr int NMT = (NSP + 31) / 32;               // 10 M tiles
-constexpr int IH = 4 * PH + 7, IW = 4 * PW + 8;    // input pixels per tile (23 x 72; col 71 feeds only
-                                                   // the zero kw = 7 tap, but must be finite)
+// 7 x 8 pooled outputs per tile: 15 x 17 = 255 stem pixels = 8 M tiles of 32, so the 16 (M, N) tiles split
+// evenly over the 8 waves (a 4 x 16 tile's 297 pixels made 10 M tiles: 3 for half the waves, 2 for the rest)
+constexpr int PH = 7, PW = 8;                      // pooled outputs per tile
+constexpr int SH = 2 * PH + 1, SW = 2 * PW + 1;    // stem pixels per tile (15 x 17)
+constexpr int NSP = SH * SW;                       // 255
+constexpr int NMT = (NSP + 31) / 32;               // 8 M tiles
+constexpr int IH = 4 * PH + 7, IW = 4 * PW + 8;    // input pixels per tile (35 x 40; the last column feeds
+                                                   // only the zero kw = 7 tap, but must be finite)
 constexpr int IP = IW;                             // LDS pitch in pixels (even)
 constexpr int KS = 14;                             // k16 steps
-constexpr int SOP = 64 + 4;                        // stem tile pitch (floats)
+constexpr int SOP = 64;                            // stem tile pitch (floats): a 16-lane ds_read_b128 group of
+                                                   // the pool (quads of pixels 2k apart) then hits 64 distinct
+                                                   // banks; the epilogue's 32-lane ds_write_b32 groups are
+                                                   // consecutive channels either way
 constexpr int NT = 512;                            // threads (8 waves)
 constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread per tile
 constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
