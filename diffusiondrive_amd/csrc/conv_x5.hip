@@ -27,6 +27,7 @@
 //    feed 384 MFMAs at 256 x 256 - half the L2 bytes per MFMA of conv_x3's 128 x 128.
 //  * XCD-aware bijective tile remap; fused epilogue (per-channel weight scale, alpha, bias,
 //    residual, ReLU, strided NHWC store, non-finite flag) as conv_x3.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -413,6 +414,13 @@ static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 // slower than conv_x3 on the GPT shapes (tools/micro/gemm_x3_bench.py) and are not routed here.
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   if (a.prec != 0 && a.prec != 1) return false;
+  if (const char* e = getenv("DDMI_X5_TILE")) {  // micro-benchmark override (tools/micro/conv_bench)
+    const int t = atoi(e);
+    if (t == 1) { launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st); return true; }   // 256 x 128
+    if (t == 2) { launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st); return true; }   // 256 x 256
+    if (t == 3) { launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st); return true; }   // 256 x 64
+    if (t == 4) { launch_x5_cfg<2, 2, 2, 2, 4>(a, M, K, st); return true; }   // 128 x 128, 4 waves
+  }
   const int64_t m256 = (M + 255) / 256;
   const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;
   if (a.Cout <= 64) {

@@ -530,6 +530,15 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   if (a.res && (a.res_sw % 4 || a.res_sh % 4 || a.res_sn % 4 || !al16(a.res))) return false;
   // int32 offsets inside the kernel (the launcher checks the 2 GiB buffer-offset bound)
   if ((int64_t)a.Nimg * a.in_sn >= (int64_t(1) << 29) || (int64_t)a.Cout * a.ldh >= (int64_t(1) << 30)) return false;
+  // 8 x 8 maps (LiDAR layer 4): one 8 x 8 tile per image, 8 waves of 32 x 32 (wave tile 32 rows x 32
+  // channels: 4 fragment reads per 3 MFMAs, the LDS keeps up at this layer's 144 K steps); 102 -> 68 us per
+  // launch against conv_x3. (The same tile on the 16 x 16 LiDAR layer-3 maps, whose 16 x 16 tiles leave half
+  // the CUs idle, measured 72 us against 61: the 10 x 10 halo per 64 pixels costs more than the idle CUs.)
+  if (a.Ho == 8 && a.Wo == 8 && a.Cout % 128 == 0) {
+    if ((int64_t)a.Nimg * (a.Cout / 128) < 128) return false;
+    launch_x6_cfg<8, 8, 128, 2, 4, 3, 4, 0>(a, st);
+    return true;
+  }
   const bool wide = a.Ho < 16;  // 8 x 32 tiles for the 8-row maps (layer4 of the image trunk)
   if (wide && a.Wo < 32) return false;
   const int64_t n_sp = (int64_t)a.Nimg * (wide ? ((a.Ho + 7) / 8) * ((a.Wo + 31) / 32)

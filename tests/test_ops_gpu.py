@@ -134,7 +134,8 @@ def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     (64, 64, 256, 64, 128, 3, 2, 1, True, False, "conv_x5<256,128>"),        # image layer2 entry, 3x3 / s2
     (64, 32, 128, 128, 256, 3, 2, 1, True, False, "conv_x5<256,256>"),       # image layer3 entry, 3x3 / s2
     (1, 160, 128, 512, 2048, 1, 1, 0, True, False, "conv_x5<256,256>"),      # GPT MLP-up at C = 512 (M = 20480)
-    (64, 8, 8, 512, 512, 3, 1, 1, True, True, "conv_x3<64,64,f16x3>"),       # LiDAR layer4 (8 x 8 maps)
+    (64, 8, 8, 512, 512, 3, 1, 1, True, True, "conv_x6<8,8,128,2,4>"),       # LiDAR layer4 (8 x 8 maps)
+    (2, 8, 8, 512, 512, 3, 1, 1, True, True, "conv_x3<64,64,f16x3>"),        # too few 8 x 8 tiles for conv_x6
 ])
 def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, route):
     """f16x3 conv at the B = 64 forward's shapes: the dispatcher must take the named kernel / tile
@@ -162,6 +163,7 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p,res,route", [
     (64, 8, 32, 512, 512, 3, 1, 1, True, "conv_x6<8,32,128,4,2,bf16>"),     # image layer4
+    (64, 8, 8, 512, 512, 3, 1, 1, True, "conv_x6<8,8,128,2,4,bf16>"),       # LiDAR layer4 (8 x 8 maps)
     (16, 32, 128, 128, 128, 3, 1, 1, True, "conv_x6<16,16,128,4,2,bf16>"),  # layer2 3x3
     (4, 64, 256, 64, 64, 3, 1, 1, False, "conv_x6<16,16,64,4,2,bf16>"),     # layer1 (8-wave BN 64 form)
     (2, 12, 70, 128, 100, 3, 1, 1, True, "conv_x6<8,32,64,4,2,bf16>"),      # ragged H / W / N, 8 x 32 tiles

@@ -35,6 +35,13 @@ static const Shape kShapes[] = {
     {"img.l2.s2", 64, 64, 256, 64, 128, 3, 2, 0},
     {"img.stem7", 64, 256, 1024, 4, 64, 7, 2, 0},
     {"gpt.mlp0", 64 * 320, 1, 1, 512, 2048, 1, 1, 0},
+    {"gpt.qkv4", 64 * 320, 1, 1, 512, 1536, 1, 1, 0},
+    {"gpt.mlp2", 64 * 320, 1, 1, 2048, 512, 1, 1, 1},
+    {"gpt.proj4", 64 * 320, 1, 1, 512, 512, 1, 1, 1},
+    {"gpt.mlp0s3", 64 * 320, 1, 1, 256, 1024, 1, 1, 0},
+    {"gpt.mlp2s3", 64 * 320, 1, 1, 1024, 256, 1, 1, 1},
+    {"gpt.qkv3", 64 * 320, 1, 1, 256, 768, 1, 1, 0},
+    {"lid.l4.3x3", 64, 8, 8, 512, 512, 3, 1, 1},
 };
 
 #define CK(x)                                                                       \
