@@ -69,6 +69,112 @@ struct ConvArgs {
   int rowmap_nimg = 0;
 };
 constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
+
+#ifdef __HIPCC__
+// Implicit-GEMM epilogue row table: element offsets of output / residual row m0 + r (r < BM) of a tile,
+// written to LDS as [BM][2] int64 (-1 output offset = row past M). One runtime-divisor (n, oh, ow)
+// decomposition per row and thread, instead of one per fragment row and pass - the division sequences
+// cost conv_x5 as many cycles as its K loop on the GPT GEMMs (K = 256 - 512).
+template <int BM, int NT>
+__device__ inline void epi_row_table(const ConvArgs& a, int m0, int M, int tid, long long* tab) {
+  for (int r = tid; r < BM; r += NT) {
+    const int m = m0 + r;
+    long long oo = -1, ro = 0;
+    if (m < M) {
+      const int ow = m % a.Wo, t2 = m / a.Wo;
+      const int oh = t2 % a.Ho, n = t2 / a.Ho;
+      oo = (long long)n * a.out_sn + (long long)oh * a.out_sh + (long long)ow * a.out_sw;
+      ro = (long long)n * a.res_sn + (long long)oh * a.res_sh + (long long)ow * a.res_sw;
+    }
+    tab[2 * r] = oo;
+    tab[2 * r + 1] = ro;
+  }
+}
+
+// Can epi_quads serve this launch? Every output / residual row starts 16-B aligned and Cout % 4 == 0.
+__device__ inline bool epi_quads_ok(const ConvArgs& a) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  auto st4 = [](int64_t s, int n) { return n == 1 || s % 4 == 0; };
+  return a.Cout % 4 == 0 && al(a.out) && al(a.wsinv) && (!a.bias || al(a.bias)) && st4(a.out_sn, a.Nimg) &&
+         st4(a.out_sh, a.Ho) && st4(a.out_sw, a.Wo) &&
+         (!a.res || (al(a.res) && st4(a.res_sn, a.Nimg) && st4(a.res_sh, a.Ho) && st4(a.res_sw, a.Wo)));
+}
+template <int WM, int WN, int TM, int TN>
+constexpr int epi_quads_lds() {  // bytes: one parked slab of every wave + the row table
+  return WM * 32 * WN * TN * 32 * 4 + WM * TM * 32 * 16;
+}
+
+// Implicit-GEMM epilogue through LDS (after the K loop, with the stage LDS free): slab i (32 rows per
+// wave row) of the WM x WN waves' 32x32 accumulators is parked as [WM*32 rows][BN] fp32, then every
+// thread finishes 16-B channel quads of whole rows - weight scale, alpha, bias, residual, ReLU - with
+// one 16-B store each. The accumulator layout's own stores (4 B per lane, 128 B per half-wave) are
+// store-issue bound: the 256 x 256 tile's 1024 of them per workgroup took as long as a K = 512 loop.
+// Parked 16-B slots are XOR-ed with bit 2 of the row (<< 3): a park store's two half-waves write rows
+// 4 apart, which then fall on opposite 32-bank halves. Returns true if an accumulator was non-finite.
+// C/D map of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+template <int WM, int WN, int TM, int TN, typename Acc>
+__device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], char* lds, int m0, int n0, int M,
+                                 int tid) {
+  typedef float f4_t __attribute__((ext_vector_type(4)));
+  constexpr int NT = 64 * WM * WN, BN = WN * TN * 32, QN = BN / 4, PR = WM * 32;
+  constexpr int RPP = NT / QN, IT = PR / RPP;  // rows per pass, quads per thread per slab
+  static_assert(NT % QN == 0 && PR % RPP == 0 && BN >= 64, "quad epilogue tiling");
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN, li = lane & 31, hh = lane >> 5;
+  float* ct = reinterpret_cast<float*>(lds);
+  long long* tab = reinterpret_cast<long long*>(lds + PR * BN * 4);
+  epi_row_table<WM * TM * 32, NT>(a, m0, M, tid, tab);
+  const int qn = tid % QN, nq = n0 + 4 * qn;
+  const bool nv = nq < a.Cout;
+  f4_t scl = {0.f, 0.f, 0.f, 0.f}, bia = {0.f, 0.f, 0.f, 0.f};
+  if (nv) {
+    scl = *reinterpret_cast<const f4_t*>(a.wsinv + nq) * a.alpha;
+    if (a.bias) bia = *reinterpret_cast<const f4_t*>(a.bias + nq);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    if (i) __syncthreads();  // every thread has read the previous slab
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const int col = (wn * TN + j) * 32 + li;
+        ct[pr * BN + ((((col >> 2) ^ (((pr >> 2) & 1) << 3))) << 2) + (col & 3)] = acc[i][j][r];
+      }
+    __syncthreads();
+    // the slab's residuals are all loaded before its first store (out may alias res)
+    f4_t rv[IT];
+    long long oo[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int pr = tid / QN + k * RPP;
+      const int tr = ((pr >> 5) * TM + i) * 32 + (pr & 31);
+      oo[k] = nv ? tab[2 * tr] : -1;
+      rv[k] = (a.res && oo[k] >= 0) ? *reinterpret_cast<const f4_t*>(a.res + tab[2 * tr + 1] + nq)
+                                    : (f4_t){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      if (oo[k] < 0) continue;
+      const int pr = tid / QN + k * RPP;
+      const f4_t c = *reinterpret_cast<const f4_t*>(ct + pr * BN + ((qn ^ (((pr >> 2) & 1) << 3)) << 2));
+      bad |= !(__builtin_isfinite(c.x) && __builtin_isfinite(c.y) && __builtin_isfinite(c.z) &&
+               __builtin_isfinite(c.w));
+      f4_t v = c * scl + bia + rv[k];
+      if (a.relu) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+      }
+      *reinterpret_cast<f4_t*>(a.out + oo[k] + nq) = v;
+    }
+  }
+  return bad;
+}
+#endif
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
 void launch_conv_x3(const ConvArgs& a, hipStream_t st);
 // Fused stem conv 7x7/2 (Cin 4, Cout 64, f16x3) + bias + ReLU + maxpool 3x3/2 into pool_out (B,Hp,Wp,64)

@@ -75,7 +75,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   constexpr int ROWB = BK * 2;                       // 64-B LDS rows (32 halfs)
   constexpr int NIMG = PREC == 0 ? 2 : 1;             // images per operand
   constexpr int STAGE = NIMG * (BM + BN) * ROWB;      // Ah, [Al], Bh, [Bl]
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  constexpr int LDS_EPI = epi_quads_lds<WM, WN, TM, TN>();
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE > LDS_EPI ? 2 * STAGE : LDS_EPI];
 
   const int tid = threadIdx.x;
   const int nblk = n_tiles_m * n_tiles_n;
@@ -367,65 +368,63 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     iteration(kc + 1, I0);
   }
 
-  // ---- fused epilogue. C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
-  // An activation beyond the fp16 range (|x| >= 65504) makes its hi part infinite, so every output
-  // it feeds becomes inf / NaN: a non-finite result raises DD_NUM_F16_OVERFLOW.
+  // ---- epilogue: 16-B quads through LDS when every row is 16-B aligned, else per accumulator element
   bool bad = false;
-  float scl_v[TN], bias_v[TN];
-  int ncol[TN];
+  if (epi_quads_ok(a)) {
+    bad = epi_quads<WM, WN, TM, TN>(a, acc, lds, m0, n0, M, tid);
+  } else {
+    // ---- fused epilogue. C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+    // An activation beyond the fp16 range (|x| >= 65504) makes its hi part infinite, so every output
+    // it feeds becomes inf / NaN: a non-finite result raises DD_NUM_F16_OVERFLOW.
+    float scl_v[TN], bias_v[TN];
+    int ncol[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    ncol[j] = n0 + (wn * TN + j) * 32 + li;
-    const bool nv = ncol[j] < a.Cout;
-    bias_v[j] = (a.bias && nv) ? a.bias[ncol[j]] : 0.f;
-    scl_v[j] = nv ? a.wsinv[ncol[j]] * a.alpha : 0.f;
-  }
-  float* out = a.out;
-  const float* res = a.res;
-  const int osh = (int)a.out_sh, osw = (int)a.out_sw;
-  const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
-  // rows (n, oh, ow) of fragment row group q of slab i
-  auto row_of = [&](int i, int q, int e, int& n, int& oh, int& ow) {
-    const int m = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh + e;
-    ow = m % a.Wo;
-    const int t2 = m / a.Wo;
-    oh = t2 % a.Ho;
-    n = t2 / a.Ho;
-    return m < M;
-  };
+    for (int j = 0; j < TN; ++j) {
+      ncol[j] = n0 + (wn * TN + j) * 32 + li;
+      const bool nv = ncol[j] < a.Cout;
+      bias_v[j] = (a.bias && nv) ? a.bias[ncol[j]] : 0.f;
+      scl_v[j] = nv ? a.wsinv[ncol[j]] * a.alpha : 0.f;
+    }
+    float* out = a.out;
+    const float* res = a.res;
+    // row offsets once per row (the stage LDS is free: every wave is past its last fragment read)
+    const long long* tab = reinterpret_cast<const long long*>(lds);
+    epi_row_table<BM, 64 * WM * WN>(a, m0, M, tid, reinterpret_cast<long long*>(lds));
+    __syncthreads();
+    auto row_at = [&](int i, int q, int e) { return ((wm * TM + i) * 32 + 8 * q + 4 * hh + e) * 2; };
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    // this 32-row slab's residuals are all loaded before its first store: out may alias res (in
-    // place x += f(x)), so loads interleaved with stores would serialise on memory latency
-    float rv[4][4][TN];
+    for (int i = 0; i < TM; ++i) {
+      // this 32-row slab's residuals are all loaded before its first store: out may alias res (in
+      // place x += f(x)), so loads interleaved with stores would serialise on memory latency
+      float rv[4][4][TN];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int n, oh, ow;
-        const bool mv = row_of(i, q, e, n, oh, ow);
-        const float* rrow = (res && mv) ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
+        for (int e = 0; e < 4; ++e) {
+          const int r2 = row_at(i, q, e);
+          const float* rrow = (res && tab[r2] >= 0) ? res + tab[r2 + 1] : nullptr;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) rv[q][e][j] = (rrow && ncol[j] < a.Cout) ? rrow[ncol[j]] : 0.f;
-      }
+          for (int j = 0; j < TN; ++j) rv[q][e][j] = (rrow && ncol[j] < a.Cout) ? rrow[ncol[j]] : 0.f;
+        }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int n, oh, ow;
-        if (!row_of(i, q, e, n, oh, ow)) continue;
-        float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
+        for (int e = 0; e < 4; ++e) {
+          const long long oo = tab[row_at(i, q, e)];
+          if (oo < 0) continue;
+          float* orow = out + oo;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if (ncol[j] < a.Cout) {
-            const float acc_v = acc[i][j][q * 4 + e];
-            bad |= !__builtin_isfinite(acc_v);
-            float v = acc_v * scl_v[j] + bias_v[j] + rv[q][e][j];
-            if (a.relu) v = fmaxf(v, 0.f);
-            orow[ncol[j]] = v;
+          for (int j = 0; j < TN; ++j) {
+            if (ncol[j] < a.Cout) {
+              const float acc_v = acc[i][j][q * 4 + e];
+              bad |= !__builtin_isfinite(acc_v);
+              float v = acc_v * scl_v[j] + bias_v[j] + rv[q][e][j];
+              if (a.relu) v = fmaxf(v, 0.f);
+              orow[ncol[j]] = v;
+            }
           }
         }
-      }
+    }
   }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }

@@ -101,6 +101,18 @@ __device__ inline bf16x8_t to_bf16x8(const float4& p, const float4& q) {
 
 }  // namespace
 
+#ifdef DDMI_X5_STAMPS
+// diagnostic build only (DDMI_BUILD_VARIANT=x5st, tools/micro/conv_bench -DX5_STAMPS): per-workgroup
+// s_memtime at start / K loop entry / K loop exit / end
+__device__ unsigned long long g_x5_st[4096 * 4];
+extern "C" int dd_x5_stamps_read(unsigned long long* h, int n) {
+  return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_x5_st), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#define X5_STAMP(k) x5st[k] = __builtin_amdgcn_s_memtime()
+#else
+#define X5_STAMP(k)
+#endif
+
 // PREC 0: f16x3; PREC 1: the bf16 mode (A converted to bf16 at fragment-read time, B = the bf16 weight
 // image, one v_mfma_f32_32x32x16_bf16 per MAC; the stage's second B image is not filled).
 template <int WM, int WN, int TM, int TN, int MODE, int NS, int PREC>
@@ -119,11 +131,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   static_assert(B_IN >= 1 && BN % (16 * NW) == 0, "B rows per wave");
   static_assert(NS >= 2 && NS * STAGE <= 160 * 1024, "stages");
   constexpr int DPC = A_IN + (PREC ? 1 : 2) * B_IN;  // DMA instructions per wave per chunk
-  __shared__ __attribute__((aligned(1024))) char lds[NS * STAGE];
+  constexpr int LDS_EPI = epi_quads_lds<WM, WN, TM, TN>();
+  __shared__ __attribute__((aligned(1024))) char lds[NS * STAGE > LDS_EPI ? NS * STAGE : LDS_EPI];
   const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
+#ifdef DDMI_X5_STAMPS
+  unsigned long long x5st[4];
+#endif
+  X5_STAMP(0);
   const int nblk = n_tiles_m * n_tiles_n;
   const int bid = blockIdx.x;
   int tile = bid;
@@ -262,6 +279,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
 #pragma unroll
   for (int u = 0; u < NS - 1; ++u) issue(u, u * KC);
   int cur = 0;  // stage of chunk kc
+  X5_STAMP(1);
   for (int kc = 0; kc < nk; ++kc) {
     // this wave's DMAs of chunk kc have landed (NS-2 younger chunks may fly), every wave's have
     // (barrier), and every wave finished reading chunk kc-1, whose stage is refilled below
@@ -321,66 +339,70 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
     }
   }
   chunk_barrier<0>();  // drain the trailing (all-OOB) DMAs before the block retires
+  X5_STAMP(2);
 
-  // ---- fused epilogue (as conv_x3). C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  // ---- epilogue: 16-B quads through LDS when every row is 16-B aligned, else per accumulator element
   bool bad = false;
-  float scl_v[TN], bias_v[TN];
-  int ncol[TN];
+  if (epi_quads_ok(a)) {
+    bad = epi_quads<WM, WN, TM, TN>(a, acc, lds, m0, n0, M, tid);
+  } else {
+    float scl_v[TN], bias_v[TN];
+    int ncol[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    ncol[j] = n0 + (wn * TN + j) * 32 + li;
-    const bool nv = ncol[j] < a.Cout;
-    bias_v[j] = (a.bias && nv) ? a.bias[ncol[j]] : 0.f;
-    scl_v[j] = nv ? a.wsinv[ncol[j]] * a.alpha : 0.f;
-  }
-  float* out = a.out;
-  const float* res = a.res;
-  const int osh = (int)a.out_sh, osw = (int)a.out_sw;
-  const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
-  // rows (n, oh, ow) of fragment row group q of slab i
-  auto row_of = [&](int i, int q, int e, int& n, int& oh, int& ow) {
-    const int m = m0 + (wm * TM + i) * 32 + 8 * q + 4 * hh + e;
-    ow = m % a.Wo;
-    const int t2 = m / a.Wo;
-    oh = t2 % a.Ho;
-    n = t2 / a.Ho;
-    return m < M;
-  };
+    for (int j = 0; j < TN; ++j) {
+      ncol[j] = n0 + (wn * TN + j) * 32 + li;
+      const bool nv = ncol[j] < a.Cout;
+      bias_v[j] = (a.bias && nv) ? a.bias[ncol[j]] : 0.f;
+      scl_v[j] = nv ? a.wsinv[ncol[j]] * a.alpha : 0.f;
+    }
+    float* out = a.out;
+    const float* res = a.res;
+    // row offsets once per row (the stage LDS is free: every wave is past its last fragment read)
+    const long long* tab = reinterpret_cast<const long long*>(lds);
+    epi_row_table<BM, 64 * WM * WN>(a, m0, M, tid, reinterpret_cast<long long*>(lds));
+    __syncthreads();
+    auto row_at = [&](int i, int q, int e) { return ((wm * TM + i) * 32 + 8 * q + 4 * hh + e) * 2; };
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    // this 32-row slab's residuals are all loaded before its first store: out may alias res (in
-    // place x += f(x)), so loads interleaved with stores would serialise on memory latency
-    float rv[4][4][TN];
+    for (int i = 0; i < TM; ++i) {
+      // this 32-row slab's residuals are all loaded before its first store: out may alias res (in
+      // place x += f(x)), so loads interleaved with stores would serialise on memory latency
+      float rv[4][4][TN];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int n, oh, ow;
-        const bool mv = row_of(i, q, e, n, oh, ow);
-        const float* rrow = (res && mv) ? res + (int64_t)n * a.res_sn + (oh * rsh + ow * rsw) : nullptr;
+        for (int e = 0; e < 4; ++e) {
+          const int r2 = row_at(i, q, e);
+          const float* rrow = (res && tab[r2] >= 0) ? res + tab[r2 + 1] : nullptr;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) rv[q][e][j] = (rrow && ncol[j] < a.Cout) ? rrow[ncol[j]] : 0.f;
-      }
+          for (int j = 0; j < TN; ++j) rv[q][e][j] = (rrow && ncol[j] < a.Cout) ? rrow[ncol[j]] : 0.f;
+        }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int n, oh, ow;
-        if (!row_of(i, q, e, n, oh, ow)) continue;
-        float* orow = out + (int64_t)n * a.out_sn + (oh * osh + ow * osw);
+        for (int e = 0; e < 4; ++e) {
+          const long long oo = tab[row_at(i, q, e)];
+          if (oo < 0) continue;
+          float* orow = out + oo;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if (ncol[j] < a.Cout) {
-            const float acc_v = acc[i][j][q * 4 + e];
-            bad |= !__builtin_isfinite(acc_v);
-            float v = acc_v * scl_v[j] + bias_v[j] + rv[q][e][j];
-            if (a.relu) v = fmaxf(v, 0.f);
-            orow[ncol[j]] = v;
+          for (int j = 0; j < TN; ++j) {
+            if (ncol[j] < a.Cout) {
+              const float acc_v = acc[i][j][q * 4 + e];
+              bad |= !__builtin_isfinite(acc_v);
+              float v = acc_v * scl_v[j] + bias_v[j] + rv[q][e][j];
+              if (a.relu) v = fmaxf(v, 0.f);
+              orow[ncol[j]] = v;
+            }
           }
         }
-      }
+    }
   }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+#ifdef DDMI_X5_STAMPS
+  __syncthreads();
+  X5_STAMP(3);
+  if (tid == 0 && blockIdx.x < 4096)
+    for (int k = 0; k < 4; ++k) g_x5_st[blockIdx.x * 4 + k] = x5st[k];
+#endif
 }
 
 template <int WM, int WN, int TM, int TN, int NS, int PREC>

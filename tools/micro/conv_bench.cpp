@@ -15,6 +15,10 @@
 
 #include "common.h"
 #include "weights.h"
+#ifdef X5_STAMPS
+#include <string>
+extern "C" int dd_x5_stamps_read(unsigned long long* h, int n);
+#endif
 
 using namespace ddmi;
 
@@ -42,6 +46,13 @@ static const Shape kShapes[] = {
     {"gpt.mlp2s3", 64 * 320, 1, 1, 1024, 256, 1, 1, 1},
     {"gpt.qkv3", 64 * 320, 1, 1, 256, 768, 1, 1, 0},
     {"lid.l4.3x3", 64, 8, 8, 512, 512, 3, 1, 1},
+    // fixed-cost probes: the img.l2 / img.l3 tiles with the K walk halved / doubled
+    {"fx.l3.c128", 64, 16, 64, 128, 256, 3, 1, 1},
+    {"fx.l3.c512", 64, 16, 64, 512, 256, 3, 1, 1},
+    {"fx.l2.c64", 64, 32, 128, 64, 128, 3, 1, 1},
+    {"fx.l2.c256", 64, 32, 128, 256, 128, 3, 1, 1},
+    {"fx.l2.nores", 64, 32, 128, 128, 128, 3, 1, 0},
+    {"fx.l3.nores", 64, 16, 64, 256, 256, 3, 1, 0},
 };
 
 #define CK(x)                                                                       \
@@ -148,6 +159,28 @@ int main(int argc, char** argv) {
     CK(hipMemset(dout, 0xff, nout * 4));  // NaN fill: a skipped output shows up
     const float ms = timed(b);
     CK(hipStreamSynchronize(st));
+#ifdef X5_STAMPS
+    {  // conv_x5 phase stamps of the last launch (diagnostic library built with DDMI_BUILD_VARIANT=x5st)
+      std::vector<unsigned long long> t(4096 * 4);
+      if (dd_x5_stamps_read(t.data(), 4096 * 4) == 0 && std::string(last_conv_kernel()) == "conv_x5") {
+        unsigned long long t0 = ~0ull, tend = 0;
+        int n = 0;
+        double pro = 0, mainl = 0, epi = 0;
+        for (int w = 0; w < 4096; ++w) {
+          if (!t[w * 4 + 3] || t[w * 4 + 3] < t[w * 4]) continue;
+          ++n;
+          t0 = std::min(t0, t[w * 4]);
+          tend = std::max(tend, t[w * 4 + 3]);
+          pro += t[w * 4 + 1] - t[w * 4];
+          mainl += t[w * 4 + 2] - t[w * 4 + 1];
+          epi += t[w * 4 + 3] - t[w * 4 + 2];
+        }
+        printf("  stamps: %d WGs  span %llu  per WG: prologue %.0f  main %.0f  epilogue %.0f (s_memtime ticks)\n", n,
+               tend - t0, pro / n, mainl / n, epi / n);
+        std::memset(t.data(), 0, t.size() * 8);
+      }
+    }
+#endif
     std::vector<float> ho(nout), hr(nout);
     CK(hipMemcpy(ho.data(), dout, nout * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(hr.data(), dref, nout * 4, hipMemcpyDeviceToHost));
