@@ -106,7 +106,10 @@ __device__ inline bf16x8_t to_bf16x8(const float4& p, const float4& q) {
 // s_memtime at start / K loop entry / K loop exit / end
 __device__ unsigned long long g_x5_st[4096 * 4];
 extern "C" int dd_x5_stamps_read(unsigned long long* h, int n) {
-  return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_x5_st), (size_t)n * 8) == hipSuccess ? 0 : -1;
+  void* d = nullptr;  // read, then clear for the next launch
+  if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_x5_st)) != hipSuccess) return -1;
+  if (hipMemcpy(h, d, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(d, 0, (size_t)n * 8) == hipSuccess ? 0 : -1;
 }
 #define X5_STAMP(k) x5st[k] = __builtin_amdgcn_s_memtime()
 #else

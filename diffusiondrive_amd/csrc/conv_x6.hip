@@ -120,6 +120,21 @@ constexpr bool halo_in_window(int t, int D, int TA, bool first) {
 
 }  // namespace
 
+#ifdef DDMI_X6_STAMPS
+// diagnostic build only (DDMI_BUILD_VARIANT=x6st, tools/micro/build_conv_bench.sh x6st): per-workgroup
+// s_memtime at start / K loop entry / K loop exit / end
+__device__ unsigned long long g_x6_st[8192 * 4];
+extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
+  void* d = nullptr;  // read, then clear for the next launch
+  if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_x6_st)) != hipSuccess) return -1;
+  if (hipMemcpy(h, d, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(d, 0, (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#define X6_STAMP(k) x6st[k] = __builtin_amdgcn_s_memtime()
+#else
+#define X6_STAMP(k)
+#endif
+
 // TH x TW output pixels x BN channels per workgroup of WM x WN waves; B ring of NSLOT slots filled
 // D steps ahead (NSLOT >= D + 1). SH = 1: ONE halo buffer (the next chunk's halo is written after a
 // barrier that retires every wave's last read of the current one), so a 4-wave BN = 64 workgroup
@@ -158,6 +173,10 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef DDMI_X6_STAMPS
+  unsigned long long x6st[4];
+#endif
+  X6_STAMP(0);
 
   // ---- tile (XCD-aware bijective remap: each XCD takes a contiguous run of tiles, N-tile major)
   const int nblk = n_sp * ntn;
@@ -417,10 +436,12 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     step(c, std::integral_constant<int, 7>(), FIRST);
     step(c, std::integral_constant<int, 8>(), FIRST);
   };
+  X6_STAMP(1);
   chunk(0, std::true_type());
   for (int c = 1; c < nchunks; ++c) chunk(c, std::false_type());
   // drain the trailing (all-OOB) DMAs and LDS reads; every wave done with the ring and the halo
   step_barrier<0>();
+  X6_STAMP(2);
 
   // ---- epilogue through LDS: the 256 x BN fp32 tile is parked as [pixel][BN], then every lane
   // finishes 16-B channel quads: weight scale, alpha, bias, residual, ReLU, one 16-B store.
@@ -487,6 +508,12 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     *reinterpret_cast<x6f4*>(out + ooff[k]) = v;
   }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+#ifdef DDMI_X6_STAMPS
+  __syncthreads();
+  X6_STAMP(3);
+  if (tid == 0 && blockIdx.x < 8192)
+    for (int k = 0; k < 4; ++k) g_x6_st[blockIdx.x * 4 + k] = x6st[k];
+#endif
 }
 
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>

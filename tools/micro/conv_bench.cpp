@@ -15,9 +15,10 @@
 
 #include "common.h"
 #include "weights.h"
-#ifdef X5_STAMPS
+#if defined(X5_STAMPS) || defined(X6_STAMPS)
 #include <string>
 extern "C" int dd_x5_stamps_read(unsigned long long* h, int n);
+extern "C" int dd_x6_stamps_read(unsigned long long* h, int n);
 #endif
 
 using namespace ddmi;
@@ -159,25 +160,31 @@ int main(int argc, char** argv) {
     CK(hipMemset(dout, 0xff, nout * 4));  // NaN fill: a skipped output shows up
     const float ms = timed(b);
     CK(hipStreamSynchronize(st));
+#if defined(X5_STAMPS) || defined(X6_STAMPS)
+    {  // per-workgroup phase stamps of the last launch (diagnostic library, DDMI_BUILD_VARIANT=x5st / x6st)
 #ifdef X5_STAMPS
-    {  // conv_x5 phase stamps of the last launch (diagnostic library built with DDMI_BUILD_VARIANT=x5st)
-      std::vector<unsigned long long> t(4096 * 4);
-      if (dd_x5_stamps_read(t.data(), 4096 * 4) == 0 && std::string(last_conv_kernel()) == "conv_x5") {
-        unsigned long long t0 = ~0ull, tend = 0;
+      const char* kname = "conv_x5";
+      auto rd = dd_x5_stamps_read;
+      const int NWG = 4096;  // g_x5_st
+#else
+      const char* kname = "conv_x6";
+      auto rd = dd_x6_stamps_read;
+      const int NWG = 8192;  // g_x6_st
+#endif
+      std::vector<unsigned long long> t(NWG * 4);
+      if (rd(t.data(), NWG * 4) == 0 && std::string(last_conv_kernel()) == kname) {
         int n = 0;
         double pro = 0, mainl = 0, epi = 0;
-        for (int w = 0; w < 4096; ++w) {
+        for (int w = 0; w < NWG; ++w) {
           if (!t[w * 4 + 3] || t[w * 4 + 3] < t[w * 4]) continue;
           ++n;
-          t0 = std::min(t0, t[w * 4]);
-          tend = std::max(tend, t[w * 4 + 3]);
           pro += t[w * 4 + 1] - t[w * 4];
           mainl += t[w * 4 + 2] - t[w * 4 + 1];
           epi += t[w * 4 + 3] - t[w * 4 + 2];
         }
-        printf("  stamps: %d WGs  span %llu  per WG: prologue %.0f  main %.0f  epilogue %.0f (s_memtime ticks)\n", n,
-               tend - t0, pro / n, mainl / n, epi / n);
-        std::memset(t.data(), 0, t.size() * 8);
+        if (n)
+          printf("  stamps: %d WGs  per WG: prologue %.0f  main %.0f  epilogue %.0f (s_memtime ticks)\n", n, pro / n,
+                 mainl / n, epi / n);
       }
     }
 #endif
