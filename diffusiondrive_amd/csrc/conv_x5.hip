@@ -68,7 +68,11 @@ __device__ inline void dma16(x5i4 rsrc, uint32_t lds_wave, uint32_t voff) {
 template <int N>
 __device__ inline void chunk_barrier() {
   static_assert(N >= 0 && N < 64, "vmcnt");
+#ifdef DDMI_X5_NOBAR  // timing diagnostic only: races by construction
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#else
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+#endif
 }
 
 // 8 fp32 -> hi / lo fp16 fragments (RNE twice)
@@ -451,6 +455,11 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   }
   const int64_t m256 = (M + 255) / 256;
   const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;
+  // 1x1 stride-1 GEMMs (the GPT M = 20480 token GEMMs): 256 x 256 tiles already pay at half a chip of
+  // tiles when Cout is a multiple of 256 from 512 up (MLP-down K = 2048: 172 -> 161 us, qkv C = 256:
+  // 52 -> 43 us, MLP-up C = 128: 34 -> 31 us), 256 x 128 for Cout = 256 k + 128 (qkv C = 128: 25 -> 23 us);
+  // Cout = 256 GEMMs with 80 tiles stay on conv_x3 (tools/micro/conv_bench, DDMI_X5_TILE)
+  const bool gemm = a.KH * a.KW == 1 && a.stride == 1;
   if (a.Cout <= 64) {
     if (m256 < 256) return false;
     launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st);  // 256 x 64, 4 waves
@@ -458,6 +467,10 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
     launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);  // 256 x 256, 8 waves
   } else if (a.Cout <= 128 && m256 * n128 >= 256) {
     launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);  // 256 x 128, 8 waves
+  } else if (gemm && a.Cout >= 512 && a.Cout % 256 == 0 && m256 * n256 >= 128) {
+    launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);
+  } else if (gemm && a.Cout % 256 == 128 && m256 * n128 >= 192) {
+    launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);
   } else {
     return false;
   }

@@ -46,6 +46,11 @@ static const Shape kShapes[] = {
     {"gpt.mlp0s3", 64 * 320, 1, 1, 256, 1024, 1, 1, 0},
     {"gpt.mlp2s3", 64 * 320, 1, 1, 1024, 256, 1, 1, 1},
     {"gpt.qkv3", 64 * 320, 1, 1, 256, 768, 1, 1, 0},
+    {"gpt.mlp0s2", 64 * 320, 1, 1, 128, 512, 1, 1, 0},
+    {"gpt.qkv2", 64 * 320, 1, 1, 128, 384, 1, 1, 0},
+    {"gpt.proj3", 64 * 320, 1, 1, 256, 256, 1, 1, 1},
+    {"img.l4.s2", 64, 16, 64, 256, 512, 3, 2, 0},
+    {"img.l4.ds", 64, 16, 64, 256, 512, 1, 2, 0},
     {"lid.l4.3x3", 64, 8, 8, 512, 512, 3, 1, 1},
     // fixed-cost probes: the img.l2 / img.l3 tiles with the K walk halved / doubled
     {"fx.l3.c128", 64, 16, 64, 128, 256, 3, 1, 1},
