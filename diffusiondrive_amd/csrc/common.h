@@ -67,6 +67,15 @@ struct ConvArgs {
   // rowmap_nimg = images in the input (operand-extent check).
   const int* rowmap = nullptr;
   int rowmap_nimg = 0;
+  // Fused GPT token pooling (conv_x6 only; launch_conv_gemm reports it through last_conv_pooled()):
+  // when pool_out is set, the mean of every pool_p x pool_p output window (after bias / residual / ReLU)
+  // plus pool_add[wy * pool_add_sh + wx * pool_add_sw + c] (if set) is also written to
+  // pool_out[n * pool_sn + wy * pool_sh + wx * pool_sw + c] - the avgpool_kernel arithmetic, same order.
+  float* pool_out = nullptr;
+  int pool_p = 0;
+  int64_t pool_sn = 0, pool_sh = 0, pool_sw = 0;
+  const float* pool_add = nullptr;
+  int64_t pool_add_sh = 0, pool_add_sw = 0;
 };
 constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
 
@@ -183,6 +192,8 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
 // name of the kernel the last conv / GEMM dispatch on this thread went to ("conv_gemm", "conv_x3",
 // "conv_x5", "conv_x6"); the runtime's profiler attributes launch time per kernel with it
 const char* last_conv_kernel();
+bool last_conv_pooled();           // did the last launch_conv_gemm also write ConvArgs::pool_out?
+void set_last_conv_pooled(bool p);
 // the kernel + tile configuration of the calling thread's last conv / GEMM launch, e.g.
 // "conv_x6<8,32,128,4,2>" (TH, TW, BN, wave grid), "conv_x5<256,256>", "conv_x3<128,128,f16x3>"
 const char* last_conv_config();

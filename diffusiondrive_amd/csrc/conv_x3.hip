@@ -459,6 +459,9 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st);                 // conv_
 static thread_local const char* g_last_conv = "conv_gemm";
 const char* last_conv_kernel() { return g_last_conv; }
 void set_last_conv_kernel(const char* k) { g_last_conv = k; }
+static thread_local bool g_last_pooled = false;
+bool last_conv_pooled() { return g_last_pooled; }
+void set_last_conv_pooled(bool p) { g_last_pooled = p; }
 static thread_local const char* g_last_cfg = "";
 const char* last_conv_config() { return g_last_cfg; }
 void set_last_conv_config(const char* c) { g_last_cfg = c; }

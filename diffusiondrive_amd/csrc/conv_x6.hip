@@ -506,6 +506,28 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
       v.w = fmaxf(v.w, 0.f);
     }
     *reinterpret_cast<x6f4*>(out + ooff[k]) = v;
+    if (a.pool_out) *reinterpret_cast<x6f4*>(ct + p * BN + 4 * qn) = v;  // the finished value, for the pool
+  }
+  if (a.pool_out) {
+    // fused GPT token pooling: every P x P window of the tile (the launcher checked that windows never
+    // straddle tiles and that tiles lie inside the map), summed dy-outer / dx-inner as avgpool_kernel
+    __syncthreads();
+    const int P = a.pool_p, WX = TW / P, NWIN = (TH / P) * WX;
+    const float inv = 1.0f / (float)(P * P);
+    for (int w = tid; w < NWIN * QN; w += NT) {
+      const int win = w / QN, q = w - win * QN;
+      const int nc = n0 + 4 * q;
+      if (nc >= a.Cout) continue;
+      const int wy = win / WX, wx = win - wy * WX;
+      x6f4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int dy = 0; dy < P; ++dy)
+        for (int dx = 0; dx < P; ++dx)
+          sum += *reinterpret_cast<const x6f4*>(ct + ((wy * P + dy) * TW + wx * P + dx) * BN + 4 * q);
+      x6f4 v = sum * inv;
+      const int py = oy0 / P + wy, px = ox0 / P + wx;
+      if (a.pool_add) v += *reinterpret_cast<const x6f4*>(a.pool_add + py * a.pool_add_sh + px * a.pool_add_sw + nc);
+      *reinterpret_cast<x6f4*>(a.pool_out + nimg * a.pool_sn + py * a.pool_sh + px * a.pool_sw + nc) = v;
+    }
   }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 #ifdef DDMI_X6_STAMPS
@@ -517,7 +539,16 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
 }
 
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
-static void launch_x6_one(const ConvArgs& a, hipStream_t st) {
+static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
+  ConvArgs a = a_in;
+  // fused token pooling: whole tiles only, windows inside tiles, 16-B aligned channel quads
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool pool = a.pool_out && a.pool_p >= 1 && TH % a.pool_p == 0 && TW % a.pool_p == 0 && a.Ho % TH == 0 &&
+                    a.Wo % TW == 0 && al16(a.pool_out) && a.pool_sn % 4 == 0 && a.pool_sh % 4 == 0 &&
+                    a.pool_sw % 4 == 0 && (!a.pool_add || (al16(a.pool_add) && a.pool_add_sh % 4 == 0 &&
+                                                           a.pool_add_sw % 4 == 0));
+  if (!pool) a.pool_out = nullptr;
+  set_last_conv_pooled(pool);
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   const int n_sp = a.Nimg * tiles_x * tiles_y;
   const int ntn = (a.Cout + BN - 1) / BN;

@@ -149,6 +149,7 @@ class Model {
   // DDMI_TFDEC_MK=0: the unfused per-op chain)
   bool tfdec_mk = true;
   bool gpt_attn_x3 = true;  // f16x3 GPT attention in the f16x3 / bf16 modes (DDMI_GPT_ATTN_X3=0: the fp32-MFMA kernel)
+  bool fuse_pool = true;    // GPT token pooling in the stage-final conv_x6 epilogue (DDMI_FUSE_POOL=0: avgpool launches)
   bool tf_mk_ready = false;
   struct TfMkW {
     MkLinOff sa_in, sa_out, ca_q, ca_out, l1, l2;
@@ -210,6 +211,7 @@ class Model {
     if (const char* e = getenv("DDMI_DECODER_MK")) decoder_mk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_TFDEC_MK")) tfdec_mk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_GPT_ATTN_X3")) gpt_attn_x3 = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_FUSE_POOL")) fuse_pool = atoi(e) != 0;
     if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
@@ -767,6 +769,20 @@ class Model {
     a.flags = num_flags;
   }
 
+  // GPT token pooling fused into the next conv's epilogue (conv_x6; see ConvArgs::pool_out): set before
+  // the conv, consumed by it; pool_done tells whether that conv wrote the tokens (otherwise the caller runs
+  // launch_avgpool, e.g. in the fp32 mode or when the conv routes elsewhere)
+  struct PoolSpec {
+    float* out = nullptr;
+    int64_t sn = 0, sh = 0, sw = 0;
+    const float* add = nullptr;
+    int64_t add_sh = 0, add_sw = 0;
+    int oh = 0, ow = 0;  // pooled grid
+  };
+  PoolSpec pool_next;
+  int pool_next_p = 0;
+  bool pool_done = false;
+
   // conv on strided NHWC views
   ConvArgs conv_args(const Conv& c, const float* in, int64_t isn, int64_t ish, int64_t isw, int N, int H, int Wd,
                      float* out, int64_t osn, int64_t osh, int64_t osw, bool relu, const float* res, int64_t rsn,
@@ -799,6 +815,17 @@ class Model {
     a.pad = c.pad;
     a.relu = relu;
     use_split(a, c.x3);
+    if (pool_next_p > 0) {
+      a.pool_out = pool_next.out;
+      a.pool_p = pool_next_p;
+      a.pool_sn = pool_next.sn;
+      a.pool_sh = pool_next.sh;
+      a.pool_sw = pool_next.sw;
+      a.pool_add = pool_next.add;
+      a.pool_add_sh = pool_next.add_sh;
+      a.pool_add_sw = pool_next.add_sw;
+      pool_next_p = 0;
+    }
     return a;
   }
   void conv(const Conv& c, const float* in, int64_t isn, int64_t ish, int64_t isw, int N, int H, int Wd, float* out,
@@ -807,6 +834,7 @@ class Model {
     ConvArgs a = conv_args(c, in, isn, ish, isw, N, H, Wd, out, osn, osh, osw, relu, res, rsn, rsh, rsw);
     const double fl = 2.0 * N * a.Ho * a.Wo * (double)c.cout * c.k * c.k * c.cin_real;
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
+    pool_done = a.pool_out && last_conv_pooled();
   }
   // timm stem conv1 / bn1 / act1 + maxpool 3x3/2: one fused kernel (stem_pool.hip) in f16x3 mode,
   // otherwise the conv into `stem` and the pool from it
@@ -911,7 +939,10 @@ class Model {
 
   // ------------------------------------------------------------------ backbone
   // one ResNet stage; x (B,H,W,Cin) contiguous -> returns output buffer, updates H/W
-  float* run_stage(const TrunkW& t, int s, const float* x, int B, int& H, int& Wd, const std::string& tag) {
+  // `pool`: token pooling of the stage output to fuse into the final conv (pooled = whether it was)
+  float* run_stage(const TrunkW& t, int s, const float* x, int B, int& H, int& Wd, const std::string& tag,
+                   const PoolSpec* pool = nullptr, bool* pooled = nullptr) {
+    if (pooled) *pooled = false;
     const std::vector<Block>& blocks = t.stages[s];
     const int stride = s == 0 ? 1 : 2;
     const int Ho = (H + 2 - 3) / stride + 1, Wo = (Wd + 2 - 3) / stride + 1;
@@ -936,14 +967,24 @@ class Model {
         conv_c(blk.ds, cur, B, ch, cw, dsb, false);
         sc = dsb;
       }
+      const bool last = b + 1 == blocks.size();
+      auto request_pool = [&]() {  // square windows that tile the output exactly
+        if (!last || !pool || oh % pool->oh || ow % pool->ow || oh / pool->oh != ow / pool->ow) return;
+        pool_next = *pool;
+        pool_next_p = oh / pool->oh;
+      };
       if (!blk.bottleneck) {
         conv_c(blk.c1, cur, B, ch, cw, tmp2, true);
+        request_pool();
         conv_c(blk.c2, tmp2, B, oh, ow, y, true, sc);
       } else {
         conv_c(blk.c1, cur, B, ch, cw, tmp1, true);
         conv_c(blk.c2, tmp1, B, ch, cw, tmp2, true);
+        request_pool();
         conv_c(blk.c3, tmp2, B, oh, ow, y, true, sc);
       }
+      if (last && pool && pooled) *pooled = pool_done;
+      pool_next_p = 0;
       cur = y;
       ch = oh;
       cw = ow;
@@ -954,7 +995,34 @@ class Model {
   }
 
   // GPT fusion at scale i (transfuser_backbone.py:241-362); img (B,Hi,Wi,C), lid (B,Hl,Wl,Cl) in place.
-  void fuse(int i, float* imgf, int B, int Hi, int Wi, float* lidf, int Hl, int Wl) {
+  // the GPT token buffers of scale i (also the fused-pool targets of the stage's final convs)
+  PoolSpec img_pool_spec(int i, int B) {
+    const int C = gpt[i].C, T = 320;
+    PoolSpec p;
+    p.out = buf("gpt_x", (size_t)B * T * C);
+    p.sn = (int64_t)T * C;
+    p.sh = (int64_t)32 * C;
+    p.sw = C;
+    p.add = W(gpt[i].pos);
+    p.add_sh = (int64_t)32 * C;
+    p.add_sw = C;
+    p.oh = 8;
+    p.ow = 32;
+    return p;
+  }
+  PoolSpec lid_pool_spec(int i, int B) {
+    const int Cl = lid.ch[1 + i];
+    PoolSpec p;
+    p.out = buf("gpt_lpool", (size_t)B * 64 * Cl);
+    p.sn = (int64_t)64 * Cl;
+    p.sh = (int64_t)8 * Cl;
+    p.sw = Cl;
+    p.oh = 8;
+    p.ow = 8;
+    return p;
+  }
+  void fuse(int i, float* imgf, int B, int Hi, int Wi, float* lidf, int Hl, int Wl, bool img_pooled = false,
+            bool lid_pooled = false) {
     const GptW& g = gpt[i];
     const int C = g.C, Cl = lid.ch[1 + i];
     const int T = 320, nimg = 256;
@@ -968,9 +1036,9 @@ class Model {
     float* LO = buf("gpt_lout", (size_t)B * 64 * Cl);
     // tokens: pooled image (8x32) + pos_emb, then lidar_channel_to_img(pooled lidar 8x8) + pos_emb
     View4 xo{X, (int64_t)T * C, (int64_t)32 * C, C, 1};
-    launch("pool", 0, [&] { launch_avgpool(imgf, B, Hi, Wi, C, 8, 32, xo, W(g.pos), st); });
+    if (!img_pooled) launch("pool", 0, [&] { launch_avgpool(imgf, B, Hi, Wi, C, 8, 32, xo, W(g.pos), st); });
     View4 lpo{LP, (int64_t)64 * Cl, (int64_t)8 * Cl, Cl, 1};
-    launch("pool", 0, [&] { launch_avgpool(lidf, B, Hl, Wl, Cl, 8, 8, lpo, nullptr, st); });
+    if (!lid_pooled) launch("pool", 0, [&] { launch_avgpool(lidf, B, Hl, Wl, Cl, 8, 8, lpo, nullptr, st); });
     conv(l2i[i], LP, (int64_t)64 * Cl, (int64_t)8 * Cl, Cl, B, 8, 8, X + (size_t)nimg * C, (int64_t)T * C,
          (int64_t)8 * C, C, false, W(g.pos) + (size_t)nimg * C, 0, (int64_t)8 * C, C);
     const int M = B * T;
@@ -1079,10 +1147,13 @@ class Model {
     int Hi = hi2, Wi = wi2, Hl = hl2, Wl = wl2;
     for (int s = 0; s < 4; ++s) {
       if (s > 0) fork();
-      side([&] { xl = run_stage(lid, s, xl, B, Hl, Wl, "lid"); });
-      xi = run_stage(img, s, xi, B, Hi, Wi, "img");
+      // the stages' final convs also write the GPT tokens (fused pooling) where conv_x6 runs them
+      const PoolSpec ip = img_pool_spec(s, B), lp = lid_pool_spec(s, B);
+      bool ipooled = false, lpooled = false;
+      side([&] { xl = run_stage(lid, s, xl, B, Hl, Wl, "lid", fuse_pool ? &lp : nullptr, &lpooled); });
+      xi = run_stage(img, s, xi, B, Hi, Wi, "img", fuse_pool ? &ip : nullptr, &ipooled);
       join();
-      fuse(s, xi, B, Hi, Wi, xl, Hl, Wl);
+      fuse(s, xi, B, Hi, Wi, xl, Hl, Wl, ipooled, lpooled);
     }
     alias("img_l4", xi);
     alias("bev_feature", xl);  // (B, 8, 8, 512) NHWC; transformer_decoder_join -> fused = lidar (:204-205)

@@ -382,3 +382,39 @@ def test_tf_decoder_megakernel_matches_unfused_chain(gpu_model, seeded_sd, monke
     lines.append(f"  trajectory waypoint L2 {l2:.3e}")
     _report(lines)
     assert l2 <= WAYPOINT_L2_TOL
+
+
+def test_fused_token_pooling_matches_avgpool(gpu_model, seeded_sd, monkeypatch):
+    """The GPT token pooling of every scale (adaptive avg-pool of the stage output to 8 x 32 / 8 x 8 tokens,
+    + pos_emb; transfuser_backbone.py:241-276) runs inside the stage-final conv_x6 epilogue where conv_x6
+    takes that conv; DDMI_FUSE_POOL=0 keeps the separate avgpool launches. Same arithmetic in the same
+    order, so the forward is unchanged (1e-6); and the fused path is proven taken (fewer pool launches)."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 4
+    inp = synthetic_inputs(B, 41)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"])
+    gpu_model.set_gemm_mode("f16x3")
+    try:
+        gpu_model.set_profiling(True)
+        gpu_model.reset_stats()
+        res = gpu_model.forward(feats, noise=nz)
+        out = res["trajectory"].numpy()
+        pools = gpu_model.kernel_stats("pool")["launches"]
+        sizes = {"bev_feature": B * 64 * 512, "cross_in": B * 4096 * 320, "gpt_x": B * 320 * 512}
+        taps = {k: gpu_model.tap(k).cpu().numpy()[:n] for k, n in sizes.items()}
+    finally:
+        gpu_model.set_profiling(False)
+        gpu_model.set_gemm_mode("fp32")
+    monkeypatch.setenv("DDMI_FUSE_POOL", "0")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+    m.set_profiling(True)
+    ref = m.forward(feats, noise=nz)
+    ref_pools = m.kernel_stats("pool")["launches"]
+    m.set_profiling(False)
+    assert ref_pools == 8, ref_pools  # 4 scales x (image, LiDAR)
+    assert pools < ref_pools, (pools, ref_pools)
+    for k, v in taps.items():
+        assert float(np.abs(m.tap(k).cpu().numpy()[: v.size] - v).max()) <= 1e-6, k
+    assert waypoint_l2(out, ref["trajectory"].numpy()) <= 1e-6
