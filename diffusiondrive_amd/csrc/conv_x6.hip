@@ -80,7 +80,11 @@ __device__ inline x6f4 vload6(x6i4 rsrc, uint32_t voff) {
 template <int N>
 __device__ inline void step_barrier() {
   static_assert(N >= 0 && N < 64, "vmcnt");
+#ifdef DDMI_X6_NOBAR  // timing diagnostic only (variant build x6nb): races by construction
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+#else
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+#endif
 }
 
 template <int N>

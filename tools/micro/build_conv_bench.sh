@@ -6,6 +6,15 @@
 #     per-workgroup prologue / K loop / epilogue s_memtime split per shape (x6st: the same for conv_x6)
 set -e
 R=$(cd "$(dirname "$0")/../.." && pwd)
+if [ -n "${1:-}" ] && [ "${1:-}" != "x5st" ] && [ "${1:-}" != "x6st" ]; then
+  # any other library variant (DDMI_BUILD_VARIANT=$1): the same benchmark against libddmi_$1.so
+  V=$1
+  mkdir -p "$R/tools/micro/$V"
+  /opt/rocm/bin/hipcc -O2 -std=c++17 --offload-arch=gfx950 -I "$R/diffusiondrive_amd/csrc" -I "$R/include" \
+    "$R/tools/micro/conv_bench.cpp" -L "$R/diffusiondrive_amd" -l:libddmi_$V.so \
+    -Wl,-rpath,'$ORIGIN/../../../diffusiondrive_amd' -o "$R/tools/micro/$V/conv_bench"
+  exit 0
+fi
 if [ "${1:-}" = "x5st" ] || [ "${1:-}" = "x6st" ]; then
   V=$1
   mkdir -p "$R/tools/micro/$V"
