@@ -89,6 +89,8 @@ _SIGS = {
     "dd_op_softmax_rows": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, c_void_p]),
     "dd_op_bilinear": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
                                       ctypes.c_int, ctypes.c_int, c_void_p]),
+    "dd_op_bilinear_add": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
+                                          ctypes.c_int, ctypes.c_int, c_void_p]),
     "dd_op_maxpool3x3s2": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           c_void_p, c_void_p]),
     "dd_op_avgpool": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -36,6 +36,7 @@
 
 #include "common.h"
 
+
 namespace ddmi {
 
 namespace {
@@ -461,9 +462,11 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
   // the residual / scale / bias loads go out before the accumulators are parked, so their latency
   // hides under the LDS staging and its barrier (when the per-thread residual fits beside the
-  // accumulators: 8 quads; 4-wave workgroups load it after the barrier)
+  // accumulators; 4-wave workgroups load it after the barrier)
   constexpr int IT = BM / (NT / QN);  // pixels per thread
-  constexpr bool EARLY = IT <= 8;
+  // (8-wave workgroups: up to 16 quads - the fragment / halo registers are dead by now; ~1 % on the BN = 128
+  // layers, same-box A/B)
+  constexpr bool EARLY = IT <= (NW == 8 ? 16 : 8);
   x6f4 rv[IT];
   int ooff[IT];
   auto load_res = [&]() {

@@ -176,6 +176,53 @@ __global__ void bilinear_kernel(View4 in, int Hi, int Wi, int C, View4 out, int 
   }
 }
 
+// VEC = 4 upsample-add over HBM-sized maps: 4 channel vectors per thread (block-strided), every destination
+// load issued before the first is used (4x the bytes in flight of bilinear_kernel<4>'s one per thread); the
+// per-element arithmetic is bilinear_kernel<4>'s, so the result is bit-identical.
+constexpr int kBlU = 4;
+__global__ __launch_bounds__(256) void bilinear_add4_kernel(View4 in, int Hi, int Wi, int C, View4 out, int Ho,
+                                                            int Wo, float rh, float rw) {
+  const int b = blockIdx.z, y = blockIdx.y;
+  int y0, y1;
+  float ly0, ly1;
+  bl_index(y, rh, Hi, y0, y1, ly0, ly1);
+  const int CV = C / 4;
+  const int n = Wo * CV;
+  const float* __restrict__ base = in.p + (int64_t)b * in.sn;
+  float* __restrict__ obase = out.p + (int64_t)b * out.sn + (int64_t)y * out.sh;
+  const int i0 = blockIdx.x * (256 * kBlU) + threadIdx.x;
+  float4 p[kBlU];
+#pragma unroll
+  for (int u = 0; u < kBlU; ++u) {
+    const int i = i0 + u * 256;
+    const int x = i / CV, c = (i - x * CV) * 4;
+    p[u] = i < n ? *reinterpret_cast<const float4*>(obase + (int64_t)x * out.sw + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < kBlU; ++u) {
+    const int i = i0 + u * 256;
+    if (i >= n) break;
+    const int x = i / CV, c = (i - x * CV) * 4;
+    int x0, x1;
+    float lx0, lx1;
+    bl_index(x, rw, Wi, x0, x1, lx0, lx1);
+    const float4 v00 = *reinterpret_cast<const float4*>(base + y0 * in.sh + x0 * in.sw + c);
+    const float4 v01 = *reinterpret_cast<const float4*>(base + y0 * in.sh + x1 * in.sw + c);
+    const float4 v10 = *reinterpret_cast<const float4*>(base + y1 * in.sh + x0 * in.sw + c);
+    const float4 v11 = *reinterpret_cast<const float4*>(base + y1 * in.sh + x1 * in.sw + c);
+    float4 v;
+    v.x = ly0 * (lx0 * v00.x + lx1 * v01.x) + ly1 * (lx0 * v10.x + lx1 * v11.x);
+    v.y = ly0 * (lx0 * v00.y + lx1 * v01.y) + ly1 * (lx0 * v10.y + lx1 * v11.y);
+    v.z = ly0 * (lx0 * v00.z + lx1 * v01.z) + ly1 * (lx0 * v10.z + lx1 * v11.z);
+    v.w = ly0 * (lx0 * v00.w + lx1 * v01.w) + ly1 * (lx0 * v10.w + lx1 * v11.w);
+    v.x = p[u].x + v.x;
+    v.y = p[u].y + v.y;
+    v.z = p[u].z + v.z;
+    v.w = p[u].w + v.w;
+    *reinterpret_cast<float4*>(obase + (int64_t)x * out.sw + c) = v;
+  }
+}
+
 void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float ratio_h,
                      float ratio_w, int accumulate, hipStream_t st) {
   if (Ho > 65535 || B > 65535) throw std::runtime_error("bilinear: Ho / B > 65535");
@@ -185,6 +232,14 @@ void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, 
                    in.sn % 4 == 0 && out.sh % 4 == 0 && out.sw % 4 == 0 && out.sn % 4 == 0 &&
                    reinterpret_cast<uintptr_t>(in.p) % 16 == 0 && reinterpret_cast<uintptr_t>(out.p) % 16 == 0;
   const int n = Wo * (vec ? C / 4 : C);
+  // the in-place upsample-add onto a separate map (GPT fusion back into the trunks): the wide-issue form
+  const bool sep = in.p + (int64_t)B * in.sn <= out.p || out.p + (int64_t)B * out.sn <= in.p;
+  if (vec && accumulate && sep) {
+    dim3 g4((n + 256 * kBlU - 1) / (256 * kBlU), Ho, B);
+    hipLaunchKernelGGL(bilinear_add4_kernel, g4, dim3(256), 0, st, in, Hi, Wi, C, out, Ho, Wo, ratio_h, ratio_w);
+    DD_HIP_CHECK(hipGetLastError());
+    return;
+  }
   dim3 grid((n + 255) / 256, Ho, B);
   if (vec)
     hipLaunchKernelGGL(bilinear_kernel<4>, grid, dim3(256), 0, st, in, Hi, Wi, C, out, Ho, Wo, ratio_h, ratio_w,

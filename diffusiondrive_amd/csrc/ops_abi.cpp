@@ -307,6 +307,14 @@ int dd_op_bilinear(const float* in, int B, int Hi, int Wi, int C, float* out, in
   });
 }
 
+int dd_op_bilinear_add(const float* in, int B, int Hi, int Wi, int C, float* out, int Ho, int Wo, void* stream) {
+  return op_guard([&] {
+    View4 a{const_cast<float*>(in), (int64_t)Hi * Wi * C, (int64_t)Wi * C, C, 1};
+    View4 o{out, (int64_t)Ho * Wo * C, (int64_t)Wo * C, C, 1};
+    launch_bilinear(a, B, Hi, Wi, C, o, Ho, Wo, (float)Hi / (float)Ho, (float)Wi / (float)Wo, 1, S(stream));
+  });
+}
+
 int dd_op_maxpool3x3s2(const float* in, int B, int H, int W, int C, float* out, void* stream) {
   return op_guard([&] {
     const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;

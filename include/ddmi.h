@@ -183,6 +183,9 @@ int dd_op_layernorm(const float* x, const float* res, int res_div, const float* 
                     const float* film_scale, const float* film_shift, float* y, int rows, int C, void* stream);
 int dd_op_softmax_rows(float* x, int rows, int L, float scale, void* stream);
 int dd_op_bilinear(const float* in, int B, int Hi, int Wi, int C, float* out, int Ho, int Wo, void* stream);
+/* out += bilinear(in) (NHWC): the GPT-fusion upsample-add back into the trunks (transfuser_backbone.py:241-276,
+ * F.interpolate(..., mode="bilinear", align_corners=False) then `+`) */
+int dd_op_bilinear_add(const float* in, int B, int Hi, int Wi, int C, float* out, int Ho, int Wo, void* stream);
 int dd_op_maxpool3x3s2(const float* in, int B, int H, int W, int C, float* out, void* stream);
 int dd_op_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow, float* out, void* stream);
 int dd_op_bev_sample_attn(const float* logits, const float* pts, const float* value, float* out, int B, int Q,

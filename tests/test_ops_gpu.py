@@ -315,6 +315,20 @@ def test_bilinear(gpu, B, Hi, Wi, C, Ho, Wo):
     close(out.permute(0, 3, 1, 2), ref, 1e-6)
 
 
+@pytest.mark.parametrize("B,Hi,Wi,C,Ho,Wo", [(2, 8, 32, 64, 64, 256), (3, 8, 8, 128, 32, 32), (2, 8, 32, 512, 8, 32),
+                                             (1, 8, 8, 12, 16, 16), (1, 8, 32, 36, 13, 50)])
+def test_bilinear_add(gpu, B, Hi, Wi, C, Ho, Wo):
+    """The trunk upsample-add (wide-issue bilinear_add4_kernel for float4 channels, the scalar form otherwise):
+    bit-identical to base + F.interpolate's fp32 value computed in the same order."""
+    x = rnd(B, C, Hi, Wi, seed=28)
+    base = rnd(B, C, Ho, Wo, seed=29)
+    ref = base + F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=False)
+    out = g(base.permute(0, 2, 3, 1))
+    xd = g(x.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_bilinear_add(xd.data_ptr(), B, Hi, Wi, C, out.data_ptr(), Ho, Wo, None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 1e-6)
+
+
 def test_maxpool(gpu):
     x = rnd(2, 64, 37, 50, seed=19)
     ref = F.max_pool2d(x, 3, 2, 1)
