@@ -5,13 +5,13 @@
 // The unfused path writes the 64-channel stem map (1.07 GB at B = 64 for the camera) and reads it
 // back for the pool; here a workgroup owns a PH x PW tile of POOLED outputs, computes the
 // (2PH+1) x (2PW+1) stem pixels under it (the pool windows overlap by one stem row / column, which
-// is recomputed: 14 %), keeps them in LDS and writes only the pooled map.
+// is recomputed: 17 % at the 5 x 8 tile), keeps them in LDS and writes only the pooled map.
 //
 // Arithmetic: f16x3 as conv_x3.hip (fp32 operands split into fp16 hi + lo, products al*bh + ah*bl +
 // ah*bh on v_mfma_f32_32x32x16_f16, fp32 accumulation, per-channel power-of-two weight scale undone
 // in the epilogue, non-finite accumulators raise DD_NUM_F16_OVERFLOW), or (PREC 1, the bf16 mode) one
 // bf16 product per MAC on v_mfma_f32_32x32x16_bf16 from the bf16 weight image.
-//  * GEMM view per tile: M = stem pixels (255 -> 8 tiles of 32), N = 64 channels (2 tiles),
+//  * GEMM view per tile: M = stem pixels (187 -> 6 tiles of 32), N = 64 channels (2 tiles),
 //    K = 7 kh x 8 kw x 4 ch = 224 (kw = 7 is a zero tap): 14 k16 steps, each = one kernel row kh and
 //    four consecutive taps = 4 consecutive input pixels of that row.
 //  * A: the (4PH+7) x (4PW+8) input patch is split once into fp16 hi / lo images in LDS (8 B per
@@ -24,9 +24,9 @@
 //    are written as 0: every pool window holds at least one real pixel, all >= 0 after the ReLU, so
 //    0 stands in for the pool's -inf padding), then the 3 x 3 / 2 max over float4 channel quads and
 //    one 16-B store per pooled pixel quad.
-//  * Persistent grid (one 8-wave workgroup per CU, ~111 KB LDS); the next tile's input patch is
+//  * Persistent grid (two 4-wave workgroups per CU, 66 KB LDS each); the next tile's input patch is
 //    loaded into registers while the current tile's MFMAs run.
-// Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.14 x recompute,
+// Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.17 x recompute,
 // 224 / 196 K padding; HBM traffic = the input once (+ halo re-reads) + the pooled map.
 #include "common.h"
 
@@ -41,9 +41,12 @@ typedef float sp_f16 __attribute__((ext_vector_type(16)));
 typedef __bf16 sp_b8 __attribute__((ext_vector_type(8)));
 typedef __bf16 sp_b4 __attribute__((ext_vector_type(4)));
 
-// 7 x 8 pooled outputs per tile: 15 x 17 = 255 stem pixels = 8 M tiles of 32, so the 16 (M, N) tiles split
-// evenly over the 8 waves (a 4 x 16 tile's 297 pixels made 10 M tiles: 3 for half the waves, 2 for the rest)
-constexpr int PH = 7, PW = 8;                      // pooled outputs per tile
+// 5 x 8 pooled outputs per tile: 11 x 17 = 187 stem pixels = 6 M tiles of 32, so the 12 (M, N) tiles split
+// evenly over 4 waves (3 each). 4-wave workgroups with 66 KB of LDS run two per CU, whose phases drift apart, so
+// one's stem-tile epilogue and pool overlap the other's MFMAs: 0.73 -> 0.70 ms per forward against the 8-wave
+// 7 x 8 tile (255 stem pixels, one workgroup per CU; same-box bench A/B). (A 4 x 16 tile's 297 pixels made 10 M
+// tiles: 3 for half the waves, 2 for the rest.)
+constexpr int PH = 5, PW = 8;                      // pooled outputs per tile
 constexpr int SH = 2 * PH + 1, SW = 2 * PW + 1;    // stem pixels per tile (15 x 17)
 constexpr int NSP = SH * SW;                       // 255
 constexpr int NMT = (NSP + 31) / 32;               // 8 M tiles
@@ -55,7 +58,8 @@ constexpr int SOP = 64;                            // stem tile pitch (floats): 
                                                    // the pool (quads of pixels 2k apart) then hits 64 distinct
                                                    // banks; the epilogue's 32-lane ds_write_b32 groups are
                                                    // consecutive channels either way
-constexpr int NT = 512;                            // threads (8 waves)
+constexpr int NT = 256;                            // threads (4 waves; two workgroups per CU)
+constexpr int MSTEP = NT / 128;                    // M-tile stride of a wave (waves = 2 N halves x MSTEP)
 constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread per tile
 constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
 constexpr int LDS_BYTES = 2 * IMG_BYTES + NMT * 32 * SOP * 4;
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     tile_origin(t, b, py0, px0);
     const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;
     // ---- stem GEMM: wave (nt, mg) takes M tiles mg, mg + 4, mg + 8
-    for (int m = mg; m < NMT; m += 4) {
+    for (int m = mg; m < NMT; m += MSTEP) {
       const int p = min(m * 32 + li, NSP - 1);
       const int ly = p / SW, lx = p - (p / SW) * SW;
       const int base = (2 * ly) * IP + 2 * lx + 2 * hl;  // input pixel of (kh 0, kw 2h)
@@ -235,7 +239,8 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   int dev = 0, cus = 256;
   DD_HIP_CHECK(hipGetDevice(&dev));
   DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int grid = ntiles < cus ? ntiles : cus;
+  const int per_cu = NT == 512 ? 1 : 2;
+  const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
   static bool attr[2] = {false, false};
   auto go = [&](auto kern) {
     if (!attr[a.prec]) {

@@ -11,17 +11,18 @@ from diffusiondrive_amd import _lib  # noqa: E402
 
 lib = _lib.load()
 B, T = 64, 320
+PREC = int(os.environ.get("ATTN_PREC", "1"))  # 1: the f16x3 kernel (default mode), 0: fp32 MFMA
 for C in (64, 128, 256, 512):
     qkv = torch.randn(B, T, 3 * C, device="cuda")
     y = torch.empty(B, T, C, device="cuda")
     for _ in range(3):
-        _lib.check(lib.dd_op_gpt_attention(qkv.data_ptr(), y.data_ptr(), B, T, C, 4, None), lib, op=True)
+        _lib.check(lib.dd_op_gpt_attention(qkv.data_ptr(), y.data_ptr(), B, T, C, 4, PREC, None), lib, op=True)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n = 20
     e0.record()
     for _ in range(n):
-        lib.dd_op_gpt_attention(qkv.data_ptr(), y.data_ptr(), B, T, C, 4, None)
+        lib.dd_op_gpt_attention(qkv.data_ptr(), y.data_ptr(), B, T, C, 4, PREC, None)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
