@@ -24,6 +24,12 @@
 #include <cstdlib>
 
 #include "common.h"
+
+// f16x3 GPT attention, waves per workgroup (the largest divisor of T / 32 up to): 10 for head sizes <= 64 - one
+// workgroup per (scene, head) at T = 320, so each K / V tile is split and staged once, not twice (hs 64:
+// 59 -> 42 us, hs 16 / 32: -11 %; tools/micro/attn_bench.py, same box); 5 at hs = 128, whose 10-wave form spills
+#define DDMI_ATTN_NW 10
+#define DDMI_ATTN_NW128 5
 #include "mk_core.h"
 
 namespace ddmi {
@@ -212,7 +218,8 @@ __global__ __launch_bounds__(256) void gpt_attn_kernel(const float* __restrict__
 
 // ---------------------------------------------------------------------------------------------------
 // f16x3 form (the f16x3 / bf16 modes): NW waves per workgroup, one per 32-query block (T / 32 NW
-// workgroups per (scene, head); NW = 5 at T = 320 keeps <= 256 VGPRs per wave), flash-style over 32-key
+// workgroups per (scene, head); at T = 320 NW = 10 for hs <= 64, 5 for hs = 128, whose 10-wave form spills),
+// flash-style over 32-key
 // tiles staged in LDS already split (K three ways as key rows, V two ways transposed to dimension rows;
 // double-buffered at hs <= 32, single at 64 / 128 so 2-3 workgroups share a CU), so no wave splits an
 // operand element more than once:
@@ -488,11 +495,12 @@ void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, floa
   if (heads <= 0 || C % heads) throw std::runtime_error("gpt_attention: C % heads != 0");
   const int hs = C / heads;
   if (prec != 0) {
-    // f16x3 form: T % 32 == 0, NW (waves per workgroup) = the largest divisor of T / 32 that is <= 5
+    // f16x3 form: T % 32 == 0, NW (waves per workgroup) = the largest divisor of T / 32 that is <= DDMI_ATTN_NW
+    // (DDMI_ATTN_NW128 at hs = 128)
     if (T % 32 || T > 1024 || (reinterpret_cast<uintptr_t>(qkv) & 15) || C % 4)
       throw std::runtime_error("gpt_attention(f16x3): T % 32 == 0, T <= 1024, 16-B aligned qkv, C % 4 == 0");
     const int nq = T / 32;
-    int nw = 5;
+    int nw = hs >= 128 ? DDMI_ATTN_NW128 : DDMI_ATTN_NW;
     while (nq % nw) --nw;
     const float scale = (float)(1.0 / std::sqrt((double)hs));
     const dim3 grid((unsigned)((int64_t)B * heads * (nq / nw))), block((unsigned)(64 * nw));
@@ -500,6 +508,7 @@ void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, floa
     auto go = [&](auto HSC) {
       constexpr int HS = decltype(HSC)::value;
       switch (nw) {
+        case 10: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 10>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
         case 5: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 5>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
         case 4: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 4>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
         case 3: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 3>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
