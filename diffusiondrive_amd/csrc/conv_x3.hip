@@ -493,13 +493,7 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
   if (a.rowmap) {
     g_last_conv = "conv_x3";
-#if defined(DDMI_GATHER_X3) && DDMI_GATHER_X3 == 1
-    launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // experiment: 64 x 64
-#elif defined(DDMI_GATHER_X3) && DDMI_GATHER_X3 == 2
-    launch_x3_cfg<2, 2, 2, 1>(a, M, K, st);  // experiment: 128 x 64
-#else
     launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);  // gathered rows: 128 x 128
-#endif
     return;
   }
   if (launch_conv_x6(a, st)) {
