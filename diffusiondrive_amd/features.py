@@ -56,11 +56,22 @@ def _stage(dev: torch.device, kind: str, numel: int, dtype: torch.dtype) -> torc
     return ent[0]
 
 
+_copy_streams: Dict[int, torch.cuda.Stream] = {}
+
+
 def _upload(dev: torch.device, kind: str, host: torch.Tensor, shape) -> torch.Tensor:
-    """Asynchronous H2D copy of the staged bytes on the current stream; marks the stage busy until it lands."""
-    d = host.view(*shape).to(dev, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record(torch.cuda.current_stream(dev))
+    """Asynchronous H2D copy of the staged bytes on a copy stream of its own (so it overlaps a forward still
+    running on the compute stream), which the current stream then waits for; the stage stays busy until it lands."""
+    cs = _copy_streams.get(dev.index)
+    if cs is None:
+        cs = _copy_streams[dev.index] = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    with torch.cuda.stream(cs):
+        d = host.view(*shape).to(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(cs)
+    cur.wait_event(ev)
+    d.record_stream(cur)
     _stages[(dev.index, kind)][1] = ev
     return d
 

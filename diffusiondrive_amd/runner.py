@@ -38,33 +38,63 @@ class BatchedTrajectoryRunner:
         self.builder = TransfuserFeatureBuilder(agent._config, device=self.device)
         self.failed: List[Tuple[str, str]] = []
 
-    def _run_batch(self, tokens: List[str], inputs: List) -> Dict[str, Trajectory]:
+    def _features(self, inputs: List):
+        """The batch's device features and its DDIM start noise (one draw per batch, in batch order)."""
         cfg = self.agent._config
         feats = self.builder.compute_features_batch(inputs)
         noise = torch.randn((len(inputs), cfg.num_modes, cfg.trajectory_sampling.num_poses, 2))
-        with torch.no_grad():
-            out = self.agent._transfuser_model.forward(feats, noise=noise, safe=True)
+        return feats, noise
+
+    def _finish(self, job) -> Dict[str, Trajectory]:
+        """Wait for a launched batch; if its forward raised a numerics flag, re-run it the safe way (fp32)."""
+        tokens, feats, noise, out = job
+        model = self.agent._transfuser_model
+        if model.numerics_flags(clear=True):
+            with torch.no_grad():
+                out = model.forward(feats, noise=noise, safe=True)
         poses = out["trajectory"].cpu().numpy()
         return {t: Trajectory(np.ascontiguousarray(poses[i])) for i, t in enumerate(tokens)}
 
+    def _run_batches(self, batches: Iterable[Tuple[List[str], List]]) -> Dict[str, Trajectory]:
+        """Software-pipelined: batch i+1's host-side feature staging (the raw-sensor copy into the pinned
+        stage) runs while batch i's forward is on the GPU; batch i is then finished (synchronised, its numerics
+        flag read - the feature kernels raise none) before batch i+1's forward is launched, so every flag
+        belongs to one forward."""
+        model = self.agent._transfuser_model
+        out: Dict[str, Trajectory] = {}
+        prev = None
+        for tokens, inputs in batches:
+            feats, noise = self._features(inputs)
+            if prev is not None:
+                out.update(self._finish(prev))
+            else:
+                model.numerics_flags(clear=True)
+            with torch.no_grad():
+                res = model.forward(feats, noise=noise, safe=False)
+            prev = (tokens, feats, noise, res)
+        if prev is not None:
+            out.update(self._finish(prev))
+        return out
+
     def run(self, tokens: Iterable[str], get_agent_input: Callable[[str], object]) -> Dict[str, Trajectory]:
         """{token: Trajectory} for every token whose input loads; failures land in ``self.failed``."""
-        out: Dict[str, Trajectory] = {}
-        pend_t, pend_i = [], []
-        for tok in tokens:
-            try:
-                ai = get_agent_input(tok)
-            except Exception as e:  # noqa: BLE001 - the reference marks the token invalid and goes on
-                self.failed.append((tok, repr(e)))
-                continue
-            pend_t.append(tok)
-            pend_i.append(ai)
-            if len(pend_t) == self.batch_size:
-                out.update(self._run_batch(pend_t, pend_i))
-                pend_t, pend_i = [], []
-        if pend_t:
-            out.update(self._run_batch(pend_t, pend_i))
-        return out
+        def batches():
+            pend_t, pend_i = [], []
+            for tok in tokens:
+                try:
+                    ai = get_agent_input(tok)
+                except Exception as e:  # noqa: BLE001 - the reference marks the token invalid and goes on
+                    self.failed.append((tok, repr(e)))
+                    continue
+                pend_t.append(tok)
+                pend_i.append(ai)
+                if len(pend_t) == self.batch_size:
+                    yield pend_t, pend_i
+                    pend_t, pend_i = [], []
+            if pend_t:
+                yield pend_t, pend_i
+
+        return self._run_batches(batches())
 
     def run_distributed(self, tokens: List[str], get_agent_input: Callable[[str], object],
                         group=None) -> Dict[str, Trajectory]:
