@@ -55,7 +55,9 @@ constexpr int IH = 4 * PH + 7, IW = 4 * PW + 8;    // input pixels per tile (35 
 // LDS pitch in pixels: even (a k-step's 2-pixel fragment is 16-B aligned at every kernel row) and = 2 (mod 16): a
 // lane's fragment slot is then p + ly (mod 16) for stem pixel p = 17 ly + lx, so a 16-lane ds_read_b128 group
 // crossing a stem row collides on at most one slot pair (IP = 40: shift 7 per row); -1.5 % stem time, same-box A/B.
-// (The kernel's PMC bank-conflict share, 0.38-0.40 of LDS cycles, did not move with it: its source is elsewhere.)
+// (The kernel's PMC bank-conflict share stays 0.38: a 16-lane group still spans two stem rows. A rotated layout that
+// removes the conflicts entirely measured 6 % slower - the per-read address arithmetic costs more than the LDS
+// cycles it saves)
 constexpr int IP = 50;
 constexpr int KS = 14;                             // k16 steps
 constexpr int SOP = 64;                            // stem tile pitch (floats): a 16-lane ds_read_b128 group of
