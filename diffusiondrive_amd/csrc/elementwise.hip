@@ -176,10 +176,10 @@ __global__ void bilinear_kernel(View4 in, int Hi, int Wi, int C, View4 out, int 
   }
 }
 
-// VEC = 4 upsample-add over HBM-sized maps: 4 channel vectors per thread (block-strided), every destination
-// load issued before the first is used (4x the bytes in flight of bilinear_kernel<4>'s one per thread); the
+// VEC = 4 upsample-add over HBM-sized maps: kBlU channel vectors per thread (block-strided), every destination
+// load issued before the first is used (kBlU x the bytes in flight of bilinear_kernel<4>'s one per thread); the
 // per-element arithmetic is bilinear_kernel<4>'s, so the result is bit-identical.
-constexpr int kBlU = 4;
+constexpr int kBlU = 2;  // vectors per thread (same-box bench A/B: 2 -5 % against 4, 8 +4 %)
 __global__ __launch_bounds__(256) void bilinear_add4_kernel(View4 in, int Hi, int Wi, int C, View4 out, int Ho,
                                                             int Wo, float rh, float rw) {
   const int b = blockIdx.z, y = blockIdx.y;
