@@ -221,6 +221,29 @@ def test_stem_pool_bf16(gpu, B, H, W):
     close(out.permute(0, 3, 1, 2), ref, 1e-4)
 
 
+@pytest.mark.parametrize("scale", [2.0 ** -6, 2.0 ** -10])
+def test_conv2d_f16x3_small_activations(gpu, scale):
+    """The f16x3 subnormal-lo regime: activations well below 2^-3 have a lo part below fp16's
+    smallest normal (2^-14), rounded to the subnormal spacing 2^-24, i.e. an absolute operand error <= 2^-25 - against
+    max|x| = scale that is a relative 2^-25 / scale (2^-19 at 2^-6, 2^-15 at 2^-10). The conv through conv_x6 must stay
+    within that bound (x sqrt(K) accumulation headroom) of the fp64 result."""
+    B, H, W, Cin, Cout = 2, 32, 32, 64, 64
+    x = rnd(B, Cin, H, W, seed=41).abs() * scale
+    w = rnd(Cout, Cin, 3, 3, seed=42, scale=1.0 / np.sqrt(Cin * 9))
+    ref = F.conv2d(x.double(), w.double(), None, 1, 1)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), None, None, out.data_ptr(), Cout, 3, 3, 1,
+                           1, 0, 0, flags.data_ptr(), None), gpu)
+    assert gpu.dd_op_last_kernel().decode().startswith("conv_x6")
+    rel = float((out.permute(0, 3, 1, 2).double().cpu() - ref).abs().max() / ref.abs().max())
+    bound = max(3e-5, 2.0 ** -25 / scale * np.sqrt(Cin * 9) / 4)
+    print(f"small activations: scale {scale:g} rel {rel:.3g} bound {bound:.3g}")
+    assert rel <= bound, (scale, rel, bound)
+    assert int(flags.item()) == 0
+
+
 def test_conv2d_f16x3_flags_overflow(gpu):
     """An activation beyond the fp16 range must raise DD_NUM_F16_OVERFLOW_BIT (never pass silently)."""
     x = rnd(1, 32, 8, 8, seed=15)
