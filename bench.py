@@ -65,7 +65,7 @@ OTHER_KERNELS = ("stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool"
 DTYPE = {
     "fp32": "fp32",
     "f16x3": "fp32 via f16x3 (each fp32 operand = hi+lo fp16, products ah*bh+ah*bl+al*bh, fp32 accumulate)",
-    "bf16": "bf16 (one bf16 product per MAC, fp32 accumulate; reduced precision)",
+    "bf16": "bf16 backbone (one bf16 product per MAC, fp32 accumulate; reduced precision), f16x3 after it",
 }
 
 
@@ -77,7 +77,8 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="scenes per GPU")
     p.add_argument("--denoise-steps", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", default="8,16", help="thread counts of the CPU-oracle baseline")
+    p.add_argument("--cpu-threads", default="", help="extra thread counts of the CPU-oracle baseline (1 rep each; "
+                                                      "the job's CPU share always runs, 3 reps)")
     p.add_argument("--arch", default="resnet34")
     p.add_argument("--gemm", default="f16x3", choices=["fp32", "f16x3", "bf16"],
                    help="conv/linear arithmetic: fp32 MFMA, the fp32-class 3-product fp16 split, or bf16")
@@ -242,14 +243,19 @@ def main():
                "bytes_per_step": int(sum(v.numel() * 4 for v in host.values()) + host_nz.numel() * 4),
                "note": "inputs copied host(pinned)->HBM inside every step; not the headline value"}
 
-    traffic = None
+    # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary (FETCH_SIZE x2 +
+    # WRITE_SIZE in separate passes over this same bench command, tools/pmc_traffic.py); the algorithmic
+    # bytes per launch come from this run's launch shapes (input map + output + residual + weight image once)
+    traffic, pmc_meta = None, {}
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{main_k}_{args.gemm}.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pmc_meta = json.load(f)
+            traffic = pmc_meta.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    algo_bytes = st["bytes"] / max(st["launches"], 1)
 
     result = {
         "metric": METRIC,
@@ -275,6 +281,9 @@ def main():
             "parallelism": f"dp{world} (scene sharding, RCCL all_gather of trajectories)",
             "graph": True,
             "gemm": args.gemm,
+            "heads": False,
+            "heads_note": "the timed forward is the waypoint path (trajectory out); the BEV-semantic and agent "
+                          "heads (off that path, 0.33 GFLOP/scene, SURVEY §8a-a10) are not run - parity tests run them",
         },
         "roofline": {
             "kernel": KERNEL_DESC[main_k],
@@ -293,7 +302,10 @@ def main():
             "sustained_note": "measured f16 32x32x16 MFMA loop on random data, whole chip: 1600 TF "
                               "(profiles/round2_h_mfma_shape.txt); peak/frac stay on the nominal ceiling",
             "traffic": traffic,
-            "traffic_source": os.path.relpath(pmc_path, ROOT) if traffic is not None else None,
+            "traffic_source": (f"{os.path.relpath(pmc_path, ROOT)} (measured {pmc_meta.get('measured', '?')}, "
+                               f"{pmc_meta.get('source', '?')})") if traffic is not None else None,
+            "algorithmic_bytes_per_launch": round(algo_bytes),
+            "traffic_over_algorithmic": round(traffic / algo_bytes, 3) if traffic and algo_bytes else None,
             "launches_per_step": st["launches"] // prof_steps,
             "avg_launch_ms": round(avg_ms, 5),
             "gflop_per_launch": round(flops_per_launch / 1e9, 4),
@@ -301,6 +313,7 @@ def main():
             "conv_kernels": {k: {"launches_per_step": v["launches"] // prof_steps,
                                  "avg_launch_ms": round(v["ms"] / max(v["launches"], 1), 5),
                                  "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] else None,
+                                 "algorithmic_mb_per_launch": round(v["bytes"] / max(v["launches"], 1) / 1e6, 2),
                                  "share_of_device_time": round(v["ms"] / total_prof_ms, 4) if total_prof_ms else None}
                              for k, v in conv_stats.items() if v["launches"]},
         },
@@ -344,32 +357,60 @@ def waypoint_l2(a, b):
     return float(np.sqrt((d ** 2).sum(-1)).max())
 
 
+def cpu_share():
+    """Host threads this job may use: min(sched affinity, the cgroup CPU quota, $OMP_NUM_THREADS) - the GPU box
+    shows the whole machine's CPUs to nproc / os.cpu_count() but grants one job a share of them."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    share = min(v for v in (aff, quota, omp) if v is not None)
+    return share, {"sched_getaffinity": aff, "cgroup_cpu_max": quota, "OMP_NUM_THREADS": omp,
+                   "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(args, cfg, sd, inp):
-    """Golden-pinned CPU oracle timed on this host: B = 64 (the metric's batch, one rep) and B = 1
-    (three reps) at each thread count of --cpu-threads. Returns (record, oracle trajectories of the
-    B = 64 sample)."""
+    """Golden-pinned CPU oracle timed on this host at the job's CPU share (cpu_share): B = 64 (the metric's
+    batch, 3 timed reps after a B = 1 warm-up) and B = 1 (3 reps); --cpu-threads adds other thread counts.
+    Returns (record, oracle trajectories of the B = 64 sample)."""
     from oracle.model import OracleModel
     om = OracleModel(sd, cfg)
     S = inp["status_feature"].shape[0]
     keys = ("camera_feature", "lidar_feature", "status_feature", "noise")
+    REPS = 3
 
     def run(n):
         return om.forward(*(inp[k][:n] for k in keys), steps=args.denoise_steps, heads=False)["trajectory"].numpy()
 
-    threads = [int(t) for t in args.cpu_threads.split(",") if t]
+    share, share_src = cpu_share()
+    threads = [share] + [int(t) for t in args.cpu_threads.split(",") if t and int(t) != share]
     grid, ref = {}, None
     for n_t in threads:
         torch.set_num_threads(n_t)
         run(1)  # warm-up
         t0 = time.perf_counter()
-        for _ in range(3):
+        for _ in range(REPS):
             run(1)
-        b1 = 3 / (time.perf_counter() - t0)
-        t0 = time.perf_counter()
-        ref = run(S)
-        bs = S / (time.perf_counter() - t0)
-        grid[f"threads={n_t}"] = {f"B={S}": round(bs, 4), "B=1": round(b1, 4)}
-    head = max(threads)
+        b1 = REPS / (time.perf_counter() - t0)
+        reps = REPS if n_t == share else 1
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = run(S)
+            times.append(time.perf_counter() - t0)
+            if ref is None:
+                ref = r
+        bs = S / float(np.median(times))
+        grid[f"threads={n_t}"] = {f"B={S}": round(bs, 4), "B=1": round(b1, 4), f"B={S}_reps": reps,
+                                  f"B={S}_s_per_rep": [round(t, 3) for t in times]}
+    head = share
     cpu_name = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -384,9 +425,10 @@ def cpu_baseline(args, cfg, sd, inp):
         "unit": "scenes/s",
         "cores": head,
         "kind": "port",
-        "sample": f"{S} scenes x 1 rep (and 1 scene x 3 reps) of the same synthetic batch per thread count "
+        "sample": f"the timed {S}-scene batch x {REPS} reps (median rep; and 1 scene x {REPS} reps) at {head} threads "
                   f"(oracle/model.py, PyTorch-CPU fp32, {cpu_name}; {os.cpu_count()} host CPUs visible, "
-                  f"{head} = this job's CPU share)",
+                  f"{head} = this job's CPU share: min of the sources in cpu_share)",
+        "cpu_share": share_src,
         "grid": grid,
     }
     return rec, ref

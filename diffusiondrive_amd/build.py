@@ -20,7 +20,7 @@ ARCH = os.environ.get("DDMI_ARCH", "gfx950")
 # megakernel records per-phase clock stamps (tools/debug/mk_stamps.py); the product library has none.
 # DDMI_BUILD_VARIANT=x5st / x6st: conv_x5 / conv_x6 per-workgroup phase stamps (tools/micro/build_conv_bench.sh)
 VARIANT = os.environ.get("DDMI_BUILD_VARIANT", "")
-LIB = os.path.join(HERE, "libddmi.so" if not VARIANT else f"libddmi_{VARIANT}.so")
+LIB = os.path.join(HERE, "libddmi.so") if not VARIANT else os.path.join(HERE, "_variants", f"libddmi_{VARIANT}.so")
 VARIANT_FLAGS = {"": [], "stamps": ["-DDDMI_MK_STAMPS"], "nopv": ["-DDDMI_MK_STAMPS", "-DDDMI_MK_NOPV"], "x5st": ["-DDDMI_X5_STAMPS"], "x6st": ["-DDDMI_X6_STAMPS"], "nobar": ["-DDDMI_X5_NOBAR", "-DDDMI_X5_STAMPS"], "x6nb": ["-DDDMI_X6_NOBAR"]}[VARIANT]
 SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "decoder_mk.hip", "tfdec_mk.hip", "bevproj.hip", "attention.hip", "stem_pool.hip", "features.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
@@ -67,6 +67,7 @@ def _compile(hipcc, src, hdr):
 def build(verbose: bool = True) -> str:
     hipcc = _hipcc()
     os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     hdr = _headers_digest()
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(lambda s: _compile(hipcc, s, hdr), SOURCES))

@@ -500,8 +500,9 @@ void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, floa
     if (T % 32 || T > 1024 || (reinterpret_cast<uintptr_t>(qkv) & 15) || C % 4)
       throw std::runtime_error("gpt_attention(f16x3): T % 32 == 0, T <= 1024, 16-B aligned qkv, C % 4 == 0");
     const int nq = T / 32;
+    // the largest instantiated wave count (10, 5, 4, 3, 2, 1) <= the cap that divides T / 32
     int nw = hs >= 128 ? DDMI_ATTN_NW128 : DDMI_ATTN_NW;
-    while (nq % nw) --nw;
+    while (nw > 1 && (nq % nw || (nw > 5 && nw != 10))) --nw;
     const float scale = (float)(1.0 / std::sqrt((double)hs));
     const dim3 grid((unsigned)((int64_t)B * heads * (nq / nw))), block((unsigned)(64 * nw));
     const size_t lds = (size_t)(hs >= 64 ? 1 : 2) * (3 * 32 * (hs + 8) + 2 * hs * 36) * 2 + (size_t)nw * 32 * sizeof(float);
@@ -513,7 +514,8 @@ void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, floa
         case 4: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 4>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
         case 3: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 3>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
         case 2: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 2>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
-        default: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 1>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+        case 1: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 1>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+        default: throw std::runtime_error("gpt_attention(f16x3): no kernel for " + std::to_string(nw) + " waves");
       }
     };
     switch (hs) {

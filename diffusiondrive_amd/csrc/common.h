@@ -4,6 +4,7 @@
 // the decoder read whole 1 KB rows (see DESIGN.md §Data layout).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -17,6 +18,18 @@
   } while (0)
 
 namespace ddmi {
+
+// Raise a kernel's dynamic-LDS limit to `bytes` once per device (the attribute is per device; the
+// bit of a device is claimed atomically, so two threads driving two handles each set their own).
+// `mask` is the caller's function-local static.
+inline void set_max_lds_once(std::atomic<uint64_t>& mask, const void* kernel, int bytes) {
+  int dev = 0;
+  DD_HIP_CHECK(hipGetDevice(&dev));
+  const uint64_t bit = uint64_t(1) << (dev & 63);
+  if (mask.load(std::memory_order_acquire) & bit) return;
+  DD_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  mask.fetch_or(bit, std::memory_order_acq_rel);
+}
 
 // Strided 4-D view (n, h, w, c) with element strides; c stride is sc.
 struct View4 {
@@ -230,6 +243,8 @@ void launch_softmax_rows(float* x, int64_t ld, int rows, int L, float scale, hip
 void launch_broadcast_rows(const float* src, int nsrc, float* dst, int rows, int C, hipStream_t st);
 // y = act(x) elementwise, n elements; act 0 = mish, 1 = relu.
 void launch_activation(const float* x, float* y, int64_t n, int act, hipStream_t st);
+// out[i] = N(0, 1) draw number first + i of the Philox4x32-10 / Box-Muller stream keyed by seed (n, first % 4 == 0)
+void launch_normal_philox(float* out, int64_t n, uint64_t seed, uint64_t first, hipStream_t st);
 
 // ----------------------------------------------------------------------------------------
 // Feature builder (features.hip): cams = B x 3 (l0, f0, r0) x H x W x 3 uint8 HWC -> out

@@ -443,10 +443,10 @@ static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 // slower than conv_x3 on the GPT shapes (tools/micro/gemm_x3_bench.py) and are not routed here.
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   if (a.prec != 0 && a.prec != 1) return false;
-  static const int t = [] {  // micro-benchmark override (tools/micro/conv_bench, tools/gpu_x5tile.sh)
-    const char* e = getenv("DDMI_X5_TILE");
-    return e ? atoi(e) : 0;
-  }();
+  // micro-benchmark override (tools/micro/conv_bench, tools/gpu_x5tile.sh), read per dispatch (a forward
+  // dispatches only when it is captured or run eagerly; graph replays do not come here)
+  const char* te = getenv("DDMI_X5_TILE");
+  const int t = te ? atoi(te) : 0;
   if (t) {
     if (t == 1) { launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st); return true; }   // 256 x 128
     if (t == 2) { launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st); return true; }   // 256 x 256

@@ -741,12 +741,8 @@ void launch_decoder_mk(const MkArgs& a, hipStream_t st) {
   if (a.B <= 0) return;
   if (!a.dim_t || !a.slots || !a.vrows || !a.akv || !a.ego || !a.film || !a.tfe || !a.pts || !a.imgx)
     throw std::runtime_error("decoder_mk: missing operand");
-  static bool attr = false;
-  if (!attr) {
-    DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(decoder_mk_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr;
+  set_max_lds_once(attr, reinterpret_cast<const void*>(decoder_mk_kernel), LDS_BYTES);
   hipLaunchKernelGGL(decoder_mk_kernel, dim3(a.B), dim3(NT), LDS_BYTES, st, a);
   DD_HIP_CHECK(hipGetLastError());
 }

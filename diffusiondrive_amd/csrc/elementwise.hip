@@ -477,4 +477,54 @@ void launch_activation(const float* x, float* y, int64_t n, int act, hipStream_t
   DD_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------- device normal draw (noise == NULL)
+// Philox4x32-10 (Salmon et al., SC'11) keyed by the 64-bit seed; counter (j, 0, 0, 0) for the j-th group of
+// four normals, j = first / 4 + thread. Box-Muller on u = ((x >> 8) + 1) 2^-24 in (0, 1] and v = (y >> 8) 2^-24:
+// r = sqrt(-2 ln u), normals r cos(2 pi v), r sin(2 pi v) from (x0, x1) and from (x2, x3).
+__device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+    c[0] = n0;
+    c[1] = n1;
+    c[2] = n2;
+    c[3] = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__global__ void normal_philox_kernel(float* __restrict__ out, int64_t n4, uint32_t k0, uint32_t k1, uint64_t group0) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const uint64_t g = group0 + (uint64_t)i;
+  uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), 0u, 0u};
+  philox4x32_10(c, k0, k1);
+  float4 o;
+  float* po = &o.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float u = (float)((c[2 * h] >> 8) + 1u) * 5.9604644775390625e-8f;  // 2^-24
+    const float v = (float)(c[2 * h + 1] >> 8) * 5.9604644775390625e-8f;
+    const float r = sqrtf(-2.0f * logf(u));
+    float s, co;
+    sincospif(2.0f * v, &s, &co);
+    po[2 * h] = r * co;
+    po[2 * h + 1] = r * s;
+  }
+  reinterpret_cast<float4*>(out)[i] = o;
+}
+
+void launch_normal_philox(float* out, int64_t n, uint64_t seed, uint64_t first, hipStream_t st) {
+  if (n % 4 || first % 4 || (reinterpret_cast<uintptr_t>(out) & 15))
+    throw std::runtime_error("normal_philox: n and first must be multiples of 4, out 16-B aligned");
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  hipLaunchKernelGGL(normal_philox_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, out, n4,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), first / 4);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace ddmi

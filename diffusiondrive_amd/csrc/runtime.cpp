@@ -70,16 +70,29 @@ struct DiffLayerW {
 };
 
 struct KStat {
-  double ms = 0, flops = 0;
+  double ms = 0, flops = 0, bytes = 0;
   long long n = 0;
 };
 
 struct PendingEv {
   std::string name;
-  double flops;
+  double flops, bytes;
   hipEvent_t a, b;
   std::string detail;  // launch shape (profiling only; written to $DDMI_LAUNCH_LOG)
 };
+
+// Algorithmic HBM bytes of one conv / GEMM launch: every operand touched once - the input map (or, for
+// gathered rows, the live rows' 3x3 neighbourhoods counted as one row each), the output, the residual,
+// and the weight image of the arithmetic (f16x3: hi + lo fp16 = 4 B, bf16: 2 B, fp32: 4 B per weight).
+static double conv_algo_bytes(const ConvArgs& c) {
+  const double K = (double)c.KH * c.KW * c.Cin;
+  const double rows_out = (double)c.Nimg * c.Ho * c.Wo * c.batch;
+  const double in = c.rowmap ? rows_out * c.Cin : (double)c.Nimg * c.H * c.W * c.Cin * c.batch;
+  const double out = rows_out * c.Cout;
+  const double res = c.res ? out : 0.0;
+  const double wb = (c.wh && c.prec == 1) ? 2.0 : 4.0;
+  return 4.0 * (in + out + res) + wb * (double)c.Cout * K;
+}
 
 static void trunk_channels(int arch, int ch[5], bool& bottleneck) {
   if (arch == 34) {
@@ -159,14 +172,18 @@ class Model {
   TfMkLayer* tf_mk_layers = nullptr;  // device copy of the 3 layers' megakernel parameters
   size_t dim_t_off = kNone;
   size_t mk_w_begin = 0, mk_w_end = 0;  // arena float range of the megakernel images (prefetched per forward)
-  // graph cache keyed by the forward's shape signature and the buffer generation
-  struct GraphEntry {
-    hipGraphExec_t exec = nullptr;
-    std::string key;
-  };
-  GraphEntry graph;
+  // graph cache keyed by the forward's shape signature; every entry belongs to the current buffer
+  // generation (the cache is emptied when a workspace buffer is (re)allocated: graphs hold its pointers)
+  std::map<std::string, hipGraphExec_t> graphs;
+  uint64_t graph_gen = 0;
   uint64_t generation = 0;  // bumped whenever a workspace buffer is (re)allocated
   std::set<std::string> known_shapes;
+  // a forward of more than max_chunk scenes runs as equal chunks of at most max_chunk (every kernel's 32-bit
+  // buffer offsets stay below 2 GiB up to 256 scenes; DDMI_MAX_CHUNK overrides, read at dd_create)
+  int max_chunk = 128;
+  // noise == NULL: the DDIM start noise is drawn on the device (Philox4x32-10 + Box-Muller, keyed by
+  // rng_seed; scene s of the stream since dd_set_seed takes draws [s Q P 2, (s + 1) Q P 2))
+  uint64_t rng_seed = 0, rng_next = 0;
 
   Model(const dd_config& c, const void* blob, size_t bytes, int dev) : cfg(c), device(dev) {
     DD_HIP_CHECK(hipSetDevice(device));
@@ -213,6 +230,10 @@ class Model {
     if (const char* e = getenv("DDMI_GPT_ATTN_X3")) gpt_attn_x3 = atoi(e) != 0;
     if (const char* e = getenv("DDMI_FUSE_POOL")) fuse_pool = atoi(e) != 0;
     if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_MAX_CHUNK")) {
+      max_chunk = atoi(e);
+      if (max_chunk < 1 || max_chunk > 256) throw std::invalid_argument("DDMI_MAX_CHUNK must be in [1, 256]");
+    }
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
     DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
     if (const char* g = getenv("DDMI_GEMM")) {
@@ -247,7 +268,7 @@ class Model {
   ~Model() {
     if (st_main) (void)hipStreamSynchronize(st_main);
     if (st_side) (void)hipStreamSynchronize(st_side);
-    if (graph.exec) (void)hipGraphExecDestroy(graph.exec);
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     for (auto& e : fj_ev) (void)hipEventDestroy(e);
@@ -736,7 +757,7 @@ class Model {
                std::to_string(c.stride) + " z=" + std::to_string(c.batch) + " HW=" + std::to_string(c.H) + "x" +
                std::to_string(c.W);
     }
-    pending.push_back({name, flops, a, b, detail});
+    pending.push_back({name, flops, shape ? conv_algo_bytes(*shape) : 0.0, a, b, detail});
   }
 
   void collect() {
@@ -750,7 +771,8 @@ class Model {
       s.ms += ms;
       s.n += 1;
       s.flops += p.flops;
-      if (log) fprintf(log, "%s\t%s\t%.6g\t%.6f\n", p.name.c_str(), p.detail.c_str(), p.flops, ms);
+      s.bytes += p.bytes;
+      if (log) fprintf(log, "%s\t%s\t%.6g\t%.6f\t%.6g\n", p.name.c_str(), p.detail.c_str(), p.flops, ms, p.bytes);
       ev_pool.push_back(p.a);
       ev_pool.push_back(p.b);
     }
@@ -1066,6 +1088,18 @@ class Model {
   }
 
   // ------------------------------------------------------------------ forward
+  // The bf16 mode (configs C2-bf16 / C4) is a BACKBONE mode: the trunks and the GPT fusion (60 of the 65
+  // GFLOP/scene at ResNet-34, 160 of 162 at ResNet-50) take one bf16 product per MAC; everything after them -
+  // FPN, BEV tokens, tf decoder, bev_proj, the optional heads and the trajectory head with its time MLP - runs
+  // in f16x3 (on the megakernels), so the decoder adds fp32-class rounding only to the backbone's bf16 error.
+  int head_mode() const { return gemm_mode == DD_GEMM_BF16 ? DD_GEMM_F16X3 : gemm_mode; }
+  struct ModeScope {
+    Model* m;
+    int saved;
+    ModeScope(Model* mm, int mode) : m(mm), saved(mm->gemm_mode) { m->gemm_mode = mode; }
+    ~ModeScope() { m->gemm_mode = saved; }
+  };
+
   struct Outs {
     float* traj = nullptr;
     float* modes = nullptr;
@@ -1101,6 +1135,7 @@ class Model {
     film_key = k;
   }
   void time_film(int steps) {
+    ModeScope head_scope(this, head_mode());
     const int d = 256;
     const std::vector<int> roll = denoise_timesteps(steps);
     float* te0 = buf("temb0", d);
@@ -1157,6 +1192,8 @@ class Model {
     }
     alias("img_l4", xi);
     alias("bev_feature", xl);  // (B, 8, 8, 512) NHWC; transformer_decoder_join -> fused = lidar (:204-205)
+    // everything past the backbone runs in the head arithmetic (bf16 mode: f16x3; see head_mode)
+    ModeScope head_scope(this, head_mode());
 
     // ---- BEV tokens + status -> keyval (B, 65, 256) (+= _keyval_embedding)
     float* KV = buf("keyval", (size_t)B * 65 * d);
@@ -1525,16 +1562,21 @@ class Model {
   std::map<std::string, float*> aliases;
   void alias(const std::string& name, float* p) { aliases[name] = p; }
 
-  void stage_inputs(const float* camera, const float* lidar, const float* status, const float* noise, int B) {
+  // noise == NULL: draw it on the device for scenes [scene0, scene0 + B) of the handle's stream
+  void stage_inputs(const float* camera, const float* lidar, const float* status, const float* noise, int B,
+                    uint64_t scene0) {
     float* cam4 = buf("in_cam4", (size_t)B * cfg.cam_h * cfg.cam_w * 4);
     float* lid4 = buf("in_lid4", (size_t)B * cfg.lidar_h * cfg.lidar_w * 4);
     float* st_in = buf("in_status", (size_t)B * 8);
-    float* nz = buf("in_noise", (size_t)B * cfg.num_modes * cfg.num_poses * 2);
+    const size_t per = (size_t)cfg.num_modes * cfg.num_poses * 2;
+    float* nz = buf("in_noise", (size_t)B * per);
     launch("misc", 0, [&] { launch_nchw_to_nhwc(camera, cam4, B, 3, cfg.cam_h, cfg.cam_w, 4, st); });
     launch("misc", 0, [&] { launch_nchw_to_nhwc(lidar, lid4, B, cfg.lidar_channels, cfg.lidar_h, cfg.lidar_w, 4, st); });
     DD_HIP_CHECK(hipMemcpyAsync(st_in, status, sizeof(float) * B * 8, hipMemcpyDeviceToDevice, st));
-    DD_HIP_CHECK(hipMemcpyAsync(nz, noise, sizeof(float) * B * cfg.num_modes * cfg.num_poses * 2,
-                                hipMemcpyDeviceToDevice, st));
+    if (noise)
+      DD_HIP_CHECK(hipMemcpyAsync(nz, noise, sizeof(float) * B * per, hipMemcpyDeviceToDevice, st));
+    else
+      launch("misc", 0, [&] { launch_normal_philox(nz, (int64_t)(B * per), rng_seed, scene0 * per, st); });
   }
 
   void copy_out(float* dst, const std::string& name, size_t n) {
@@ -1548,30 +1590,60 @@ class Model {
     DD_HIP_CHECK(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyDeviceToDevice, st));
   }
 
+  // The forward of B scenes. More than max_chunk scenes run as ceil(B / max_chunk) equal chunks (the last one
+  // may be shorter) through the same per-chunk path, in order on the handle's stream; every kernel of the path
+  // is per scene, so a chunked forward equals the forward of its chunks scene for scene.
   void forward(const float* camera, const float* lidar, const float* status, const float* noise, int B, int steps,
                const Outs& o, hipStream_t caller) {
     if (B <= 0) throw std::invalid_argument("batch must be positive");
     if (steps <= 0 || steps > (schedule == DD_SCHED_VANILLA ? 1000 : cfg.step_span))
       throw std::invalid_argument("steps must be in [1, step_span] (truncated) or [1, 1000] (vanilla)");
-    if (!camera || !lidar || !status || !noise || !o.traj) throw std::invalid_argument("null input/output pointer");
+    if (!camera || !lidar || !status || !o.traj) throw std::invalid_argument("null input/output pointer");
+    if (!noise && (cfg.num_modes * cfg.num_poses) % 2)
+      throw std::invalid_argument("device noise draw needs num_modes * num_poses even");
+    const int Q = cfg.num_modes, P = cfg.num_poses;
+    const int nch = (B + max_chunk - 1) / max_chunk, chunk = (B + nch - 1) / nch;
+    for (int b0 = 0; b0 < B; b0 += chunk) {
+      const int n = std::min(chunk, B - b0);
+      auto off = [&](const float* p, size_t per) { return p ? p + (size_t)b0 * per : nullptr; };
+      auto offw = [&](float* p, size_t per) { return p ? p + (size_t)b0 * per : nullptr; };
+      Outs oc;
+      oc.traj = offw(o.traj, (size_t)P * 3);
+      oc.modes = offw(o.modes, (size_t)Q * P * 3);
+      oc.cls = offw(o.cls, (size_t)Q);
+      oc.sem = offw(o.sem, (size_t)7 * (cfg.lidar_h / 2) * cfg.lidar_w);
+      oc.ag_states = offw(o.ag_states, (size_t)30 * 5);
+      oc.ag_labels = offw(o.ag_labels, (size_t)30);
+      forward_chunk(off(camera, (size_t)3 * cfg.cam_h * cfg.cam_w),
+                    off(lidar, (size_t)cfg.lidar_channels * cfg.lidar_h * cfg.lidar_w), off(status, 8),
+                    off(noise, (size_t)Q * P * 2), n, steps, oc, caller, rng_next + (uint64_t)b0);
+    }
+    if (!noise) rng_next += (uint64_t)B;
+  }
+
+  void forward_chunk(const float* camera, const float* lidar, const float* status, const float* noise, int B,
+                     int steps, const Outs& o, hipStream_t caller, uint64_t scene0) {
     DD_HIP_CHECK(hipSetDevice(device));
     // order the handle's stream after the caller's stream, run everything there, then hand back
     DD_HIP_CHECK(hipEventRecord(ev_in, caller));
     DD_HIP_CHECK(hipStreamWaitEvent(st, ev_in, 0));
     const bool heads = o.sem || o.ag_states || o.ag_labels;
     const uint64_t gen0 = generation;
-    stage_inputs(camera, lidar, status, noise, B);
+    stage_inputs(camera, lidar, status, noise, B, scene0);
     ensure_film(steps);
     if (generation != gen0) known_shapes.clear();
     const std::string key = std::to_string(B) + "/" + std::to_string(steps) + "/" + std::to_string(heads) + "/g" +
                             std::to_string(gemm_mode) + "/s" + std::to_string(schedule);
     if (use_graph && !profiling && known_shapes.count(key)) {
-      const std::string gkey = key + "#" + std::to_string(generation);
-      if (graph.key != gkey) {
-        if (graph.exec) DD_HIP_CHECK(hipGraphExecDestroy(graph.exec));
-        graph.exec = nullptr;
-        graph.key.clear();
+      if (graph_gen != generation || graphs.size() > 8) {
+        for (auto& g : graphs) DD_HIP_CHECK(hipGraphExecDestroy(g.second));
+        graphs.clear();
+        graph_gen = generation;
+      }
+      auto it = graphs.find(key);
+      if (it == graphs.end()) {
         hipGraph_t g;
+        hipGraphExec_t ex = nullptr;
         DD_HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
         try {
           forward_body(B, steps, heads);
@@ -1581,11 +1653,11 @@ class Model {
           throw;
         }
         DD_HIP_CHECK(hipStreamEndCapture(st, &g));
-        DD_HIP_CHECK(hipGraphInstantiate(&graph.exec, g, nullptr, nullptr, 0));
+        DD_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
         DD_HIP_CHECK(hipGraphDestroy(g));
-        graph.key = gkey;
+        it = graphs.emplace(key, ex).first;
       }
-      DD_HIP_CHECK(hipGraphLaunch(graph.exec, st));
+      DD_HIP_CHECK(hipGraphLaunch(it->second, st));
     } else {
       // eager run (the first call for a shape allocates every buffer; later calls are captured)
       const uint64_t gen1 = generation;
@@ -1775,6 +1847,24 @@ int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long lon
     if (total_ms) *total_ms = s.ms;
     if (launches) *launches = s.n;
     if (flops) *flops = s.flops;
+  });
+}
+
+int dd_kernel_bytes(dd_handle* h, const char* kernel, double* bytes) {
+  return guarded([&] {
+    if (!h || !kernel || !bytes) throw std::invalid_argument("null argument");
+    h->m->collect();
+    auto it = h->m->stats.find(kernel);
+    *bytes = it != h->m->stats.end() ? it->second.bytes : 0.0;
+  });
+}
+
+int dd_set_seed(dd_handle* h, unsigned long long seed) {
+  return guarded([&] {
+    if (!h) throw std::invalid_argument("null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->m->rng_seed = seed;
+    h->m->rng_next = 0;
   });
 }
 

@@ -247,13 +247,9 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int per_cu = NT == 512 ? 1 : 2;
   const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
-  static bool attr[2] = {false, false};
+  static std::atomic<uint64_t> attr[2];
   auto go = [&](auto kern) {
-    if (!attr[a.prec]) {
-      DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-      attr[a.prec] = true;
-    }
+    set_max_lds_once(attr[a.prec], reinterpret_cast<const void*>(kern), LDS_BYTES);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
                        (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
   };

@@ -376,12 +376,8 @@ void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st) {
   if (a.B <= 0) return;
   if (!a.layers || !a.qemb || !a.kvx || !a.query_out || !a.akv[0] || !a.akv[1] || !a.ego[0] || !a.ego[1])
     throw std::runtime_error("tfdec_mk: missing operand");
-  static bool attr = false;
-  if (!attr) {
-    DD_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tfdec_mk_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_T));
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr;
+  set_max_lds_once(attr, reinterpret_cast<const void*>(tfdec_mk_kernel), LDS_T);
   hipLaunchKernelGGL(tfdec_mk_kernel, dim3(a.B), dim3(NT), LDS_T, st, a);
   DD_HIP_CHECK(hipGetLastError());
 }

@@ -88,6 +88,8 @@ def camera_features(images: Sequence[Sequence[np.ndarray]], cfg: TransfuserConfi
     lib = _lib.load()
     dev = _device(device)
     B = len(images)
+    if B == 0 or any(len(sc) != 3 for sc in images):
+        raise ValueError("camera images: one (cam_l0, cam_f0, cam_r0) triple per scene, at least one scene")
     h, w = images[0][1].shape[:2]
     for sc in images:
         for im in sc:

@@ -120,26 +120,41 @@ class DiffusionDriveModel:
     def forward(self, features: Dict[str, torch.Tensor], noise: Optional[torch.Tensor] = None,
                 steps: Optional[int] = None, heads: bool = False, modes: bool = False,
                 stream: Optional[torch.cuda.Stream] = None, safe: bool = False) -> Dict[str, torch.Tensor]:
-        """``safe``: synchronise, and if a kernel raised a numerics flag (f16x3 activation beyond
+        """``noise``: the DDIM start noise (B,20,8,2); None draws it on the CPU as the reference does
+        (``torch.randn``, transfuser_model_v2.py:593); ``"device"`` lets the library draw it on the GPU
+        (Philox stream of ``set_seed``; N(0,1) but not torch.randn's values).
+        ``safe``: synchronise, and if a kernel raised a numerics flag (f16x3 activation beyond
         the fp16 range) re-run this forward in fp32 and warn; never returns a flagged result."""
         if not safe:
             return self._forward(features, noise, steps, heads, modes, stream)
+        if isinstance(noise, str):
+            raise ValueError("safe=True re-runs a flagged forward on the same noise: pass a tensor (or None)")
         if noise is None:
             B = torch.as_tensor(features["status_feature"]).shape[0]
             noise = torch.randn((B, self.config.num_modes, self.config.trajectory_sampling.num_poses, 2))
         self.numerics_flags(clear=True)
         out = self._forward(features, noise, steps, heads, modes, stream)
         if self.numerics_flags(clear=True):
-            mode = self.gemm_mode()
-            warnings.warn(f"ddmi: numerics flag raised in gemm mode {mode!r}; re-running the forward in fp32")
-            self.set_gemm_mode("fp32")
-            try:
-                out = self._forward(features, noise, steps, heads, modes, stream)
-            finally:
-                self.set_gemm_mode(mode)
-            if self.numerics_flags(clear=True):
-                raise _lib.DDMIError("numerics flag raised by the fp32 forward as well")
+            out = self.rerun_fp32(features, noise, steps, heads, modes, stream)
         return out
+
+    def rerun_fp32(self, features, noise, steps=None, heads=False, modes=False, stream=None):
+        """Re-run a forward whose numerics flag was raised directly on the fp32-MFMA path (warns; raises if
+        the fp32 forward raises a flag as well). ``noise`` must be the tensor the flagged forward used."""
+        mode = self.gemm_mode()
+        warnings.warn(f"ddmi: numerics flag raised in gemm mode {mode!r}; re-running the forward in fp32")
+        self.set_gemm_mode("fp32")
+        try:
+            out = self._forward(features, noise, steps, heads, modes, stream)
+        finally:
+            self.set_gemm_mode(mode)
+        if self.numerics_flags(clear=True):
+            raise _lib.DDMIError("numerics flag raised by the fp32 forward as well")
+        return out
+
+    def set_seed(self, seed: int):
+        """Seed of the device noise draw (``noise="device"``); restarts its stream (dd_set_seed)."""
+        _lib.check(self.lib.dd_set_seed(self.handle, int(seed) & (2 ** 64 - 1)), self.lib)
 
     def _forward(self, features, noise, steps, heads, modes, stream) -> Dict[str, torch.Tensor]:
         # stage inputs and allocate outputs on the stream the forward is ordered after, so the caching
@@ -167,9 +182,14 @@ class DiffusionDriveModel:
         if noise is None:
             # the reference draws its DDIM start noise here (transfuser_model_v2.py:593), on CPU
             noise = torch.randn((B, Q, P, 2))
-        nz = self._dev(noise)
-        if tuple(nz.shape) != (B, Q, P, 2):
-            raise ValueError(f"noise must be (B,{Q},{P},2), got {tuple(nz.shape)}")
+        if isinstance(noise, str):
+            if noise != "device":
+                raise ValueError(f"noise must be a tensor, None or 'device', got {noise!r}")
+            nz = None
+        else:
+            nz = self._dev(noise)
+            if tuple(nz.shape) != (B, Q, P, 2):
+                raise ValueError(f"noise must be (B,{Q},{P},2), got {tuple(nz.shape)}")
         dev = cam.device
         traj = torch.empty((B, P, 3), device=dev)
         outs = _lib.DDOutputs()
@@ -188,7 +208,8 @@ class DiffusionDriveModel:
             outs.bev_semantic_map = res["bev_semantic_map"].data_ptr()
             outs.agent_states = res["agent_states"].data_ptr()
             outs.agent_labels = res["agent_labels"].data_ptr()
-        _lib.check(self.lib.dd_forward_ex(self.handle, cam.data_ptr(), lid.data_ptr(), st.data_ptr(), nz.data_ptr(),
+        _lib.check(self.lib.dd_forward_ex(self.handle, cam.data_ptr(), lid.data_ptr(), st.data_ptr(),
+                                          nz.data_ptr() if nz is not None else None,
                                           B, int(steps or cfg.denoise_steps), ctypes.byref(outs),
                                           s.cuda_stream), self.lib)
         if out_device.type != "cuda":
@@ -249,4 +270,6 @@ class DiffusionDriveModel:
         ms, n, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
         _lib.check(self.lib.dd_kernel_stats(self.handle, kernel.encode(), ctypes.byref(ms), ctypes.byref(n),
                                             ctypes.byref(fl)), self.lib)
-        return {"ms": ms.value, "launches": n.value, "flops": fl.value}
+        by = ctypes.c_double()
+        _lib.check(self.lib.dd_kernel_bytes(self.handle, kernel.encode(), ctypes.byref(by)), self.lib)
+        return {"ms": ms.value, "launches": n.value, "flops": fl.value, "bytes": by.value}

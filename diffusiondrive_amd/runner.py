@@ -46,12 +46,12 @@ class BatchedTrajectoryRunner:
         return feats, noise
 
     def _finish(self, job) -> Dict[str, Trajectory]:
-        """Wait for a launched batch; if its forward raised a numerics flag, re-run it the safe way (fp32)."""
+        """Wait for a launched batch; if its forward raised a numerics flag, re-run it directly in fp32."""
         tokens, feats, noise, out = job
         model = self.agent._transfuser_model
         if model.numerics_flags(clear=True):
             with torch.no_grad():
-                out = model.forward(feats, noise=noise, safe=True)
+                out = model.rerun_fp32(feats, noise)
         poses = out["trajectory"].cpu().numpy()
         return {t: Trajectory(np.ascontiguousarray(poses[i])) for i, t in enumerate(tokens)}
 

@@ -72,6 +72,10 @@ int dd_create(const dd_config* cfg, const void* weights_blob, size_t blob_bytes,
 /* One eval forward of B scenes. Inputs are device pointers in the reference layouts:
  * camera (B,3,cam_h,cam_w), lidar (B,C,lidar_h,lidar_w), status (B,8), noise (B,Q,P,2)
  * (the DDIM start noise the reference draws with torch.randn, transfuser_model_v2.py:593).
+ * noise may be NULL: the handle then draws it on the device (Philox4x32-10 keyed by dd_set_seed's seed,
+ * Box-Muller; scene s of the handle's stream since the last dd_set_seed takes draws [s*Q*P*2, (s+1)*Q*P*2)).
+ * That draw is N(0,1) but NOT bit-equal to torch.randn's CPU stream: pass the noise explicitly to reproduce
+ * a reference run. Any B >= 1 (more than 128 scenes run as equal chunks of at most 128, same results).
  * steps = number of truncated DDIM steps (2 in the reference). out_modes / out_cls may be NULL. */
 int dd_forward(dd_handle* h, const float* camera, const float* lidar, const float* status, const float* noise,
                int B, int steps, float* out_traj, float* out_modes, float* out_cls, void* stream);
@@ -80,6 +84,10 @@ int dd_forward_ex(dd_handle* h, const float* camera, const float* lidar, const f
                   int B, int steps, const dd_outputs* outs, void* stream);
 
 int dd_destroy(dd_handle* h);
+
+/* Seed of the device noise draw (noise == NULL in dd_forward) and restart of its stream at scene 0. Default
+ * seed 0. No reference counterpart (the reference draws on the CPU, transfuser_model_v2.py:593). */
+int dd_set_seed(dd_handle* h, unsigned long long seed);
 
 /* Last error message of the calling thread ("" if none). */
 const char* dd_last_error(void);
@@ -91,6 +99,9 @@ int dd_reset_stats(dd_handle* h);
 /* Accumulated stats of one kernel class ("conv_gemm", "layernorm", ...): total device ms,
  * launches and algorithmic FLOPs (conv_gemm) since the last reset. Synchronises pending events. */
 int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long long* launches, double* flops);
+/* Algorithmic HBM bytes of the same launches (conv / GEMM classes: input map, output, residual and weight
+ * image each counted once; 0 for the other classes). */
+int dd_kernel_bytes(dd_handle* h, const char* kernel, double* bytes);
 /* Enable / disable hipGraph capture + replay of the forward (default on). */
 int dd_set_graph(dd_handle* h, int enable);
 /* GEMM arithmetic of every conv / linear of the path:
@@ -98,9 +109,10 @@ int dd_set_graph(dd_handle* h, int enable);
  *   DD_GEMM_F16X3  3-product fp16 split on f16 MFMA (conv_x3.hip): each fp32 operand becomes
  *                  hi + lo fp16, products ah*bh + ah*bl + al*bh accumulate in fp32 - fp32-class
  *                  accuracy (<= ~3*2^-22 relative per product) at 5.3x the fp32 MFMA rate.
- *   DD_GEMM_BF16   one bf16 product per MAC (operands rounded to bf16, fp32 accumulation): the
- *                  REDUCED-precision mode of the bf16 configs (BASELINE configs C2-bf16 / C4),
- *                  ~0.06-0.08 m waypoint L2 like the reference's bf16 autocast.
+ *   DD_GEMM_BF16   one bf16 product per MAC (operands rounded to bf16, fp32 accumulation) in the
+ *                  backbone (trunks + GPT fusion), f16x3 after it (FPN, BEV tokens, decoders, heads):
+ *                  the REDUCED-precision mode of the bf16 configs (BASELINE configs C2-bf16 / C4),
+ *                  held to no worse than the reference's own bf16 autocast (0.06-0.08 m).
  * Default DD_GEMM_FP32, or $DDMI_GEMM=fp32|f16x3|bf16 at dd_create. Attention score GEMMs stay fp32. */
 #define DD_GEMM_FP32 0
 #define DD_GEMM_F16X3 1

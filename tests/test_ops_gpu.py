@@ -419,7 +419,9 @@ def test_gpt_attention(gpu, B, T, C):
 
 
 @pytest.mark.parametrize("B,T,C,amp", [(2, 320, 64, 1.0), (2, 320, 128, 1.0), (1, 320, 256, 1.0), (1, 320, 512, 1.0),
-                                       (1, 320, 512, 4.0), (2, 64, 128, 1.0), (1, 96, 64, 3.0)])
+                                       (1, 320, 512, 4.0), (2, 64, 128, 1.0), (1, 96, 64, 3.0),
+                                       # T / 32 = 8, 16, 24: wave counts 4 / 4 / 4 (not the 10 of T = 320)
+                                       (1, 256, 256, 1.0), (1, 512, 128, 1.0), (1, 768, 64, 1.0), (1, 224, 512, 1.0)])
 def test_gpt_attention_f16x3(gpu, B, T, C, amp):
     """The f16x3 GPT attention (flash-style over 32-key tiles, P taken from the S^T accumulators) vs PyTorch
     fp64; amp scales q / k to sharpen the softmax (scores up to ~|40| at amp 4)."""

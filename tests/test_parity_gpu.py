@@ -173,11 +173,12 @@ def test_vanilla_ddim_schedule_matches_oracle(gpu_model, seeded_sd, mode):
     assert l2 <= WAYPOINT_L2_TOL
 
 
-# bf16 mode (configs C2-bf16 / C4: one bf16 product per MAC) is NOT a parity mode: a near-tie of the 20 cls
-# logits can flip the selected mode. Its bar is on the PRE-argmax tensors against the fp32 oracle: every
-# mode's 8 waypoints (last step, last layer; per-mode L2, max over scenes and modes), every cls logit and the
-# mode agreement (argmax equal) must be no worse than BOTH a fixed bar and the reference path's own bf16
-# (the oracle under torch.autocast(cpu, bfloat16) - the reference's bf16 class) on the same batch.
+# bf16 mode (configs C2-bf16 / C4: one bf16 product per MAC in the backbone, f16x3 after it) is NOT a parity
+# mode: a near-tie of the 20 cls logits can flip the selected mode. Its bar is on the PRE-argmax tensors against
+# the fp32 oracle: every mode's 8 waypoints (last step, last layer; per-mode L2, max over scenes and modes), every
+# cls logit and the mode agreement (argmax equal) must be no worse than BOTH a fixed bar (SURVEY §8a's measured
+# bf16-autocast class: 0.06-0.08 m) AND the reference path's own bf16 (the oracle under torch.autocast(cpu,
+# bfloat16)) on the same batch - each statistic is held to the stricter of the two.
 BF16_ALLMODE_TOL = 0.1   # m
 BF16_CLS_TOL = 0.1       # logit
 BF16_AGREE = 0.9
@@ -199,9 +200,9 @@ def _bf16_bar(out, om, args, B, tag):
     _report([f"== {tag}: all-mode waypoint L2 {st['allmode']:.3e} m (reference bf16 autocast {ac['allmode']:.3e}), "
              f"cls max dev {st['cls']:.3e} ({ac['cls']:.3e}), mode agreement {st['agree']:.3f} ({ac['agree']:.3f}), "
              f"selected-trajectory L2 {st['sel']:.3e} ({ac['sel']:.3e}) [bf16: reduced precision]"])
-    assert st["allmode"] <= max(BF16_ALLMODE_TOL, ac["allmode"]), (st, ac)
-    assert st["cls"] <= max(BF16_CLS_TOL, ac["cls"]), (st, ac)
-    assert st["agree"] >= min(BF16_AGREE, ac["agree"]), (st, ac)
+    assert st["allmode"] <= min(BF16_ALLMODE_TOL, ac["allmode"]), (st, ac)
+    assert st["cls"] <= min(BF16_CLS_TOL, ac["cls"]), (st, ac)
+    assert st["agree"] >= max(BF16_AGREE, ac["agree"]), (st, ac)
 
 
 def test_bf16_mode_resnet34(gpu_model, seeded_sd):

@@ -42,6 +42,28 @@ def test_runner_matches_per_token_compute_trajectory(gpu, seeded_sd):
 
 
 @pytest.mark.gpu
+def test_run_distributed_world1_equals_run(gpu, seeded_sd):
+    """runner.run_distributed without a process group (world 1): the whole token list on this rank, the same
+    {token: Trajectory} map as run() on the same noise stream."""
+    import torch.distributed as dist
+    from diffusiondrive_amd.agent import DiffusionDriveAgent
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.runner import BatchedTrajectoryRunner
+    assert not dist.is_initialized()
+    agent = DiffusionDriveAgent(TransfuserConfig(), device=0)
+    agent.load_state_dict(seeded_sd)
+    toks = [f"d{i}" for i in range(5)]
+    inputs = {t: make_agent_input(500 + i, n_points=4000 + 300 * i) for i, t in enumerate(toks)}
+    torch.manual_seed(21)
+    a = BatchedTrajectoryRunner(agent, batch_size=2).run_distributed(toks, inputs.__getitem__)
+    torch.manual_seed(21)
+    b = BatchedTrajectoryRunner(agent, batch_size=2).run(toks, inputs.__getitem__)
+    assert list(a) == toks and set(b) == set(toks)
+    for t in toks:
+        assert np.array_equal(a[t].poses, b[t].poses), t
+
+
+@pytest.mark.gpu
 def test_runner_matches_oracle_on_same_noise(gpu, seeded_sd):
     """The batched runner (GPU features + batched forward) against the CPU oracle: oracle features
     (oracle/features.py) and the oracle forward on the same per-scene noise the runner drew

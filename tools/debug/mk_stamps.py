@@ -4,7 +4,7 @@ import numpy as np
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 os.environ["DDMI_MK_STAMPS"] = "1"
-os.environ.setdefault("DDMI_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "diffusiondrive_amd", "libddmi_stamps.so"))
+os.environ.setdefault("DDMI_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "diffusiondrive_amd", "_variants", "libddmi_stamps.so"))
 from diffusiondrive_amd.config import TransfuserConfig
 from diffusiondrive_amd.model import DiffusionDriveModel
 from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs

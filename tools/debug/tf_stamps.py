@@ -5,7 +5,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 os.environ["DDMI_MK_STAMPS"] = "1"
-os.environ.setdefault("DDMI_LIB", os.path.join(ROOT, "diffusiondrive_amd", "libddmi_stamps.so"))
+os.environ.setdefault("DDMI_LIB", os.path.join(ROOT, "diffusiondrive_amd", "_variants", "libddmi_stamps.so"))
 from diffusiondrive_amd.config import TransfuserConfig
 from diffusiondrive_amd.model import DiffusionDriveModel
 from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs

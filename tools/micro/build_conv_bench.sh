@@ -11,16 +11,16 @@ if [ -n "${1:-}" ] && [ "${1:-}" != "x5st" ] && [ "${1:-}" != "x6st" ]; then
   V=$1
   mkdir -p "$R/tools/micro/$V"
   /opt/rocm/bin/hipcc -O2 -std=c++17 --offload-arch=gfx950 -I "$R/diffusiondrive_amd/csrc" -I "$R/include" \
-    "$R/tools/micro/conv_bench.cpp" -L "$R/diffusiondrive_amd" -l:libddmi_$V.so \
-    -Wl,-rpath,'$ORIGIN/../../../diffusiondrive_amd' -o "$R/tools/micro/$V/conv_bench"
+    "$R/tools/micro/conv_bench.cpp" -L "$R/diffusiondrive_amd/_variants" -l:libddmi_$V.so \
+    -Wl,-rpath,'$ORIGIN/../../../diffusiondrive_amd/_variants' -o "$R/tools/micro/$V/conv_bench"
   exit 0
 fi
 if [ "${1:-}" = "x5st" ] || [ "${1:-}" = "x6st" ]; then
   V=$1
   mkdir -p "$R/tools/micro/$V"
   /opt/rocm/bin/hipcc -O2 -std=c++17 -D$(echo ${V:0:2} | tr a-z A-Z)_STAMPS --offload-arch=gfx950 -I "$R/diffusiondrive_amd/csrc" \
-    -I "$R/include" "$R/tools/micro/conv_bench.cpp" -L "$R/diffusiondrive_amd" -l:libddmi_$V.so \
-    -Wl,-rpath,'$ORIGIN/../../../diffusiondrive_amd' -o "$R/tools/micro/$V/conv_bench"
+    -I "$R/include" "$R/tools/micro/conv_bench.cpp" -L "$R/diffusiondrive_amd/_variants" -l:libddmi_$V.so \
+    -Wl,-rpath,'$ORIGIN/../../../diffusiondrive_amd/_variants' -o "$R/tools/micro/$V/conv_bench"
   exit 0
 fi
 /opt/rocm/bin/hipcc -O2 -std=c++17 --offload-arch=gfx950 -I "$R/diffusiondrive_amd/csrc" -I "$R/include" \
