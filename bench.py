@@ -26,8 +26,11 @@ Rank 0 prints ONE JSON line. Besides the contract fields it reports:
   * ``whole_forward``: canonical GFLOP/scene AND the FLOPs the graph executes
     (gathered value_proj, low-res bev_proj: fewer than canonical);
   * ``cpu_baseline``: the golden-pinned CPU oracle (oracle/, PyTorch-CPU fp32) timed on this
-    host at 8 and 16 threads (the box's CPU share) on B = 64 and B = 1 samples of the same
-    workload (rank 0, N = 1 only); its outputs are the waypoint-L2 parity check of both GPU legs.
+    host at the job's CPU share (min of sched affinity, cgroup quota, $OMP_NUM_THREADS) on the
+    timed B = 64 batch (3 reps) and a B = 1 sample (rank 0, N = 1 only); its outputs are the
+    waypoint-L2 parity check of both GPU legs;
+  * ``decoder_cross_attention``: the gathered value_proj launches (the decoder's cross-BEV attention
+    contraction) with their live-row TFLOP/s.
 ``--cpu-plumbing`` (tests only) runs the launcher / gloo all_gather / max-over-ranks / JSON path
 on CPU with a stand-in step (zeros; no forward) so the multi-rank plumbing is testable here.
 """
@@ -61,7 +64,8 @@ KERNEL_DESC = {
     "conv_x6": "conv_x6 (halo-reuse direct 3x3 conv on v_mfma_f32_32x32x16_{f16 x3 | bf16})",
 }
 CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm")
-OTHER_KERNELS = ("stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample", "decoder", "tfdec", "bevproj", "misc")
+OTHER_KERNELS = ("value_proj", "stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
+                 "decoder", "tfdec", "bevproj", "misc")
 DTYPE = {
     "fp32": "fp32",
     "f16x3": "fp32 via f16x3 (each fp32 operand = hi+lo fp16, products ah*bh+ah*bl+al*bh, fp32 accumulate)",
@@ -200,13 +204,14 @@ def main():
     main_k = max(CONV_KERNELS, key=lambda k: conv_stats[k]["ms"])
     st = conv_stats[main_k]
     other = {k: model.kernel_stats(k) for k in OTHER_KERNELS}
+    value_proj = value_proj_record(model, other["value_proj"], prof_steps, B, args)
     other.update({k: v for k, v in conv_stats.items() if k != main_k})
     model.set_profiling(False)
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["flops"] / max(st["launches"], 1)
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     total_prof_ms = st["ms"] + sum(v["ms"] for v in other.values())
-    executed_flops = sum(v["flops"] for v in conv_stats.values()) + other["attn"]["flops"]
+    executed_flops = sum(v["flops"] for v in conv_stats.values()) + other["attn"]["flops"] + other["value_proj"]["flops"]
     executed_gflop_scene = executed_flops / prof_steps / B / 1e9
 
     fp32_leg = h2d = None
@@ -330,6 +335,7 @@ def main():
             "note": "canonical = SURVEY §8d algorithmic work; executed = the GEMM/conv/attention FLOPs the graph "
                     "issues (value_proj only at the sampled taps, bev_proj keyval half at 8x8)",
         },
+        "decoder_cross_attention": value_proj,
         "numerics_flags": num_flags,
     }
     if h2d is not None:
@@ -350,6 +356,31 @@ def main():
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def value_proj_record(model, vp, prof_steps, B, args):
+    """The decoder's cross-BEV attention contraction (value_proj, blocks.py:68-76,114, evaluated at the grid-sample
+    taps: the gathered conv_x3 launches). Its FLOP count in the launch stats covers every row slot (B x 640 per
+    launch); the LIVE rows are the distinct tap pixels the dedup counted (taps value_cnt_s*l* of the last profiled
+    forward, the same inputs as every profiled forward)."""
+    if not vp["launches"]:
+        return None
+    live = 0
+    for s in range(args.denoise_steps):
+        for l in range(2):
+            live += int(model.tap(f"value_cnt_s{s}l{l}")[:B].view(torch.int32).sum().item())
+    per_launch_live = live / (2 * args.denoise_steps)
+    live_flops = 2.0 * live * 256 * 2304 * prof_steps
+    sec = vp["ms"] * 1e-3
+    live_tf = live_flops / sec / 1e12
+    return {"launches_per_step": vp["launches"] // prof_steps,
+            "avg_launch_ms": round(vp["ms"] / vp["launches"], 5),
+            "slots_per_launch": B * 640, "live_rows_per_launch": round(per_launch_live, 1),
+            "live_tflops": round(live_tf, 2),
+            "live_frac_of_f16x3_ceiling": round(live_tf / ALGO_PEAK["f16x3"], 4),
+            "live_mfma_equiv_util": round(live_tf * 3 / F16_MFMA_SUSTAINED_TFLOPS, 4),
+            "note": "live_mfma_equiv_util = live-row f16 MFMA FLOP rate (3 products per MAC) / the measured sustained "
+                    "whole-chip f16 MFMA rate; the PMC MFMA-busy of the same launches is in profiles/"}
 
 
 def waypoint_l2(a, b):

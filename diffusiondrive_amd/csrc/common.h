@@ -80,6 +80,12 @@ struct ConvArgs {
   // rowmap_nimg = images in the input (operand-extent check).
   const int* rowmap = nullptr;
   int rowmap_nimg = 0;
+  // Compacted gathered rows: rowcount[n] live rows of image n sit at rowmap[n * rowcap + l], l < rowcount[n];
+  // launch row m is the m-th live row over the images in order (rows past the total are don't-care), and
+  // its output goes to row n * rowcap + l - so every tile is full except the last, and the output layout
+  // stays the per-image one the consumer indexes.
+  const int* rowcount = nullptr;
+  int rowcap = 0;
   // Fused GPT token pooling (conv_x6 only; launch_conv_gemm reports it through last_conv_pooled()):
   // when pool_out is set, the mean of every pool_p x pool_p output window (after bias / residual / ReLU)
   // plus pool_add[wy * pool_add_sh + wx * pool_add_sw + c] (if set) is also written to
@@ -97,12 +103,14 @@ constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met 
 // written to LDS as [BM][2] int64 (-1 output offset = row past M). One runtime-divisor (n, oh, ow)
 // decomposition per row and thread, instead of one per fragment row and pass - the division sequences
 // cost conv_x5 as many cycles as its K loop on the GPT GEMMs (K = 256 - 512).
+// rowidx (optional, per tile row): the output row of tile row r (< 0: none) instead of m0 + r.
 template <int BM, int NT>
-__device__ inline void epi_row_table(const ConvArgs& a, int m0, int M, int tid, long long* tab) {
+__device__ inline void epi_row_table(const ConvArgs& a, int m0, int M, int tid, long long* tab,
+                                     const int* rowidx = nullptr) {
   for (int r = tid; r < BM; r += NT) {
-    const int m = m0 + r;
+    const int m = rowidx ? rowidx[r] : m0 + r;
     long long oo = -1, ro = 0;
-    if (m < M) {
+    if (m >= 0 && m < M) {
       const int ow = m % a.Wo, t2 = m / a.Wo;
       const int oh = t2 % a.Ho, n = t2 / a.Ho;
       oo = (long long)n * a.out_sn + (long long)oh * a.out_sh + (long long)ow * a.out_sw;
@@ -136,7 +144,7 @@ constexpr int epi_quads_lds() {  // bytes: one parked slab of every wave + the r
 // C/D map of the 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
 template <int WM, int WN, int TM, int TN, typename Acc>
 __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], char* lds, int m0, int n0, int M,
-                                 int tid) {
+                                 int tid, const int* rowidx = nullptr) {
   typedef float f4_t __attribute__((ext_vector_type(4)));
   constexpr int NT = 64 * WM * WN, BN = WN * TN * 32, QN = BN / 4, PR = WM * 32;
   constexpr int RPP = NT / QN, IT = PR / RPP;  // rows per pass, quads per thread per slab
@@ -145,7 +153,7 @@ __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], ch
   const int wm = wave / WN, wn = wave % WN, li = lane & 31, hh = lane >> 5;
   float* ct = reinterpret_cast<float*>(lds);
   long long* tab = reinterpret_cast<long long*>(lds + PR * BN * 4);
-  epi_row_table<WM * TM * 32, NT>(a, m0, M, tid, tab);
+  epi_row_table<WM * TM * 32, NT>(a, m0, M, tid, tab, rowidx);
   const int qn = tid % QN, nq = n0 + 4 * qn;
   const bool nv = nq < a.Cout;
   f4_t scl = {0.f, 0.f, 0.f, 0.f}, bia = {0.f, 0.f, 0.f, 0.f};

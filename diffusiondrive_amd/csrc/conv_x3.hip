@@ -57,7 +57,7 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0>
+template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0, int GATHER = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 - a 32-wide K chunk lies inside one filter tap, the
@@ -65,7 +65,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   // MODE 0: generic K (stem 7x7 on 4 padded channels, small Cin): per-lane tap decode.
   // PREC 0: f16x3 (hi / lo images of both operands, 3 MFMA products);
   // PREC 1: bf16 (one bf16 image per operand, 1 MFMA product) - the reduced-precision mode.
+  // GATHER 1: gathered output rows (ConvArgs::rowmap, MODE 1 only), compacted over the images when
+  //           ConvArgs::rowcount is set (the decoder's value_proj at the grid-sample taps).
   constexpr int NT = 64 * WM * WN;
+  static_assert(!GATHER || MODE == 1, "gathered rows take the MODE-1 tap walk");
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int A_LD = BM * (BK / 4) / NT;  // float4 A pieces per thread per chunk
@@ -79,10 +82,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   __shared__ __attribute__((aligned(16))) char lds[2 * STAGE > LDS_EPI ? 2 * STAGE : LDS_EPI];
 
   const int tid = threadIdx.x;
+  // GATHER: g_rows[r] = the row-map index (= output row) of tile row r, -1 = none
+  __shared__ int g_rows[GATHER ? BM : 1];
+  __shared__ int g_pre[GATHER ? 257 : 1];
   const int nblk = n_tiles_m * n_tiles_n;
   const int bid = blockIdx.x;
   int tile = bid;
-  if (nblk >= 16) {
+  // (gathered rows: the live tiles are a prefix of the grid whose length only the kernel knows - the XCD remap
+  // would hand that prefix to the first XCDs alone, so consecutive tiles go round-robin over the XCDs instead)
+  if (!GATHER && nblk >= 16) {
     const int q = nblk / 8, r = nblk % 8, x = bid % 8;
     tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
@@ -90,6 +98,41 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   const int nt_idx = tile - mt_idx * n_tiles_n;
   const int m0 = mt_idx * BM;
   const int n0 = nt_idx * BN;
+  if constexpr (GATHER) {
+    if (a.rowcount) {
+      // exclusive prefix of the images' live-row counts; launch row m = the m-th live row in image order
+      const int nimg = a.rowmap_nimg;
+      for (int n = tid; n < nimg; n += NT) g_pre[n + 1] = a.rowcount[n];
+      __syncthreads();
+      if (tid == 0) {
+        int s = 0;
+        g_pre[0] = 0;
+        for (int n = 1; n <= nimg; ++n) {
+          s += g_pre[n];
+          g_pre[n] = s;
+        }
+      }
+      __syncthreads();
+      const int total = g_pre[nimg];
+      if (m0 >= total) return;  // past every live row (workgroup-uniform)
+      for (int r = tid; r < BM; r += NT) {
+        const int g = m0 + r;
+        int idx = -1;
+        if (g < total) {
+          int lo = 0, hi = nimg - 1;  // the last image whose prefix is <= g
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (g_pre[mid] <= g) lo = mid; else hi = mid - 1;
+          }
+          idx = lo * a.rowcap + (g - g_pre[lo]);
+        }
+        g_rows[r] = idx;
+      }
+    } else {
+      for (int r = tid; r < BM; r += NT) g_rows[r] = m0 + r < M ? m0 + r : -1;
+    }
+    __syncthreads();
+  }
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in);
   const __amdgpu_buffer_rsrc_t rwh = make_rsrc(a.wh);
@@ -113,9 +156,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     int oh = t2 % a.Ho;
     int n = t2 / a.Ho;
     bool rv = v;
-    if (MODE == 1 && a.rowmap) {
+    if constexpr (GATHER) {
       // gathered rows: the pixel comes from the row map (stride 1: output geometry = input's)
-      const int px = v ? a.rowmap[m] : -1;
+      const int ri = g_rows[(tid >> 3) + (NT / 8) * i];
+      const int px = ri >= 0 ? a.rowmap[ri] : -1;
       rv = px >= 0;
       any_row |= (int)rv;
       const int pp = rv ? px : 0;
@@ -141,7 +185,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   }
   // gathered rows: a tile whose rows are all don't-care (-1: the unused tail of a scene's
   // deduplicated pixel list) does no work; the predicate is workgroup-uniform
-  if (MODE == 1 && a.rowmap && !__syncthreads_or(any_row)) return;
+  if (GATHER && !__syncthreads_or(any_row)) return;
   // B rows: constant part of the byte offset and validity
   uint32_t boff[B_LD];
   bool bok[B_LD];
@@ -371,7 +415,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   // ---- epilogue: 16-B quads through LDS when every row is 16-B aligned, else per accumulator element
   bool bad = false;
   if (epi_quads_ok(a)) {
-    bad = epi_quads<WM, WN, TM, TN>(a, acc, lds, m0, n0, M, tid);
+    bad = epi_quads<WM, WN, TM, TN>(a, acc, lds, m0, n0, M, tid, GATHER ? g_rows : nullptr);
   } else {
     // ---- fused epilogue. C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5).
     // An activation beyond the fp16 range (|x| >= 65504) makes its hi part infinite, so every output
@@ -389,7 +433,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     const float* res = a.res;
     // row offsets once per row (the stage LDS is free: every wave is past its last fragment read)
     const long long* tab = reinterpret_cast<const long long*>(lds);
-    epi_row_table<BM, 64 * WM * WN>(a, m0, M, tid, reinterpret_cast<long long*>(lds));
+    epi_row_table<BM, 64 * WM * WN>(a, m0, M, tid, reinterpret_cast<long long*>(lds), GATHER ? g_rows : nullptr);
     __syncthreads();
     auto row_at = [&](int i, int q, int e) { return ((wm * TM + i) * 32 + 8 * q + 4 * hh + e) * 2; };
 #pragma unroll
@@ -429,7 +473,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int GATHER = 0>
 static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int ntm = (M + BM - 1) / BM;
@@ -440,6 +484,11 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
       "conv_x3<" + std::to_string(BM) + "," + std::to_string(BN) + ",f16x3>",
       "conv_x3<" + std::to_string(BM) + "," + std::to_string(BN) + ",bf16>"};
   set_last_conv_config(name[a.prec == 1].c_str());
+  if constexpr (GATHER) {
+    hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1, 0, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
+    DD_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (a.prec == 1) {
     if (walk)
       hipLaunchKernelGGL((conv_x3_kernel<WM, WN, TM, TN, 1, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm, ntn);
@@ -483,6 +532,8 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if (a.rowmap && (a.stride != 1 || a.Cin % BK != 0 || a.KH * a.KW > 32 || a.Nimg != 1 || a.Wo != 1 ||
                    a.rowmap_nimg < 1 || a.prec != 0))
     throw std::runtime_error("conv_x3: gathered rows need a stride-1 f16x3 MODE-1 conv into Nimg=1, Wo=1");
+  if (a.rowcount && (!a.rowmap || a.rowmap_nimg > 256 || a.rowcap < 1 || (int64_t)a.rowmap_nimg * a.rowcap > M))
+    throw std::runtime_error("conv_x3: compacted rows need a row map of <= 256 images x rowcap rows");
   const int64_t in_extent = (int64_t)((a.rowmap ? a.rowmap_nimg : a.Nimg) - 1) * a.in_sn + (int64_t)(a.H - 1) * a.in_sh +
                             (int64_t)(a.W - 1) * a.in_sw + a.Cin;
   if (in_extent * 4 >= (int64_t)kOOB || (int64_t)a.Cout * a.ldh * 2 >= (int64_t)kOOB)
@@ -493,7 +544,7 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
   if (a.rowmap) {
     g_last_conv = "conv_x3";
-    launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);  // gathered rows: 128 x 128
+    launch_x3_cfg<2, 2, 2, 2, 1>(a, M, K, st);  // gathered rows: 128 x 128
     return;
   }
   if (launch_conv_x6(a, st)) {

@@ -59,6 +59,7 @@ struct MkArgs {
   float* cls_out = nullptr;       // [B*Q]
   int* next_rows = nullptr;       // dedup tables of the next (step, layer), nullptr = none
   int* next_slots = nullptr;
+  int* next_counts = nullptr;     // [B] distinct tap pixels per scene of the next (step, layer), or nullptr
   int ddim = 0;                   // layer 1: apply the DDIM step to imgx (not the last step)
   float sa_t = 0, sb_t = 0, sa_p = 0, sdir = 0;
   float* traj = nullptr;          // layer 1 of the last step: selected trajectory [B][P][3]
@@ -74,6 +75,7 @@ struct MkInitArgs {
   float* imgx = nullptr;
   int* rows = nullptr;
   int* slots = nullptr;
+  int* counts = nullptr;  // [B] distinct tap pixels per scene, or nullptr
   float sa = 0, s1a = 0;
   int B = 0;
 };

@@ -84,9 +84,10 @@ __device__ inline void tap_geom(float tx, float ty, int& x0, int& y0, float wt[4
   wt[3] = (ix - (float)x0) * (iy - (float)y0);
 }
 
-// the scene's distinct tap pixels (pixel order) -> rows[b*cap ..], -1 past the count; each tap's
-// compact row -> slots (bev_tap_dedup_kernel's algorithm with the workgroup's threads)
-__device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int* rows, int* slots) {
+// the scene's distinct tap pixels (pixel order) -> rows[b*cap ..], -1 past the count, the count -> counts[b]
+// (the gathered value_proj compacts the scenes' rows with it); each tap's compact row -> slots
+// (bev_tap_dedup_kernel's algorithm with the workgroup's threads)
+__device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int* rows, int* slots, int* counts) {
   const int tid = threadIdx.x, nt = blockDim.x;
   constexpr int HW = kHV * kHV, cap = kQP * 4;
   const int64_t base = (int64_t)b * cap;
@@ -132,6 +133,7 @@ __device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int*
       ++r;
     }
   for (int j = total + tid; j < cap; j += nt) rows[base + j] = -1;
+  if (tid == 0 && counts) counts[b] = total;
   __syncthreads();
   for (int u = tid; u < kQP; u += nt) {
     int x0, y0;
@@ -623,7 +625,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   }
   if (a.next_rows) {
     int* table = reinterpret_cast<int*>(T1);
-    dedup_scene(SM + S_PN, table, table + 4096, b, a.next_rows, a.next_slots);
+    dedup_scene(SM + S_PN, table, table + 4096, b, a.next_rows, a.next_slots, a.next_counts);
   }
 #ifdef DDMI_MK_STAMPS
   stamp(32);
@@ -647,7 +649,7 @@ __global__ __launch_bounds__(256) void decoder_mk_init_kernel(MkInitArgs a) {
     pts[2 * t + 1] = denorm_y(fminf(fmaxf(iy, -1.f), 1.f));
   }
   __syncthreads();
-  dedup_scene(pts, table, table + 4096, b, a.rows, a.slots);
+  dedup_scene(pts, table, table + 4096, b, a.rows, a.slots, a.counts);
 }
 
 // GEMM-core test: A [32][K] fp32 -> split LDS image -> mk_gemm over 256-column units -> out

@@ -148,6 +148,8 @@ class Model {
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
   bool value_dedup = true;
+  bool value_compact = true;         // DDMI_VALUE_COMPACT=0: gathered value rows in per-scene tile runs
+  const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
   // bev_proj (DDMI_BEVPROJ): 2 "fused" = one bevproj.hip pass (f16x3 / bf16 modes; fp32 mode uses 1),
   // 1 "lowres" = keyval half at 8 x 8, upsample, K = 64 GEMM, LayerNorm; 0 "concat" = concat at 64 x 64
   int bevproj_mode = 2;
@@ -219,6 +221,7 @@ class Model {
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VALUE_COMPACT")) value_compact = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BEVPROJ")) {
       if (!strcmp(e, "fused")) bevproj_mode = 2;
       else if (!strcmp(e, "lowres")) bevproj_mode = 1;
@@ -554,7 +557,11 @@ class Model {
 
   // value_proj (3x3 conv 256 -> 256 + ReLU, blocks.py:68-76,114) of layer l evaluated only at the map
   // pixels the (step, layer)'s taps read: conv_x3 over the deduplicated row list `rows`
-  void gathered_value(int l, const int* rows, float* vrows, const float* cross, int B, int HB, int WB, int MR) {
+  // counts (nullable): the scenes' live-row counts - the launch then runs the scenes' rows compacted (full
+  // 128-row tiles; DDMI_VALUE_COMPACT=0 keeps one tile run per scene). Timed under its own class "value_proj";
+  // its FLOPs count every row slot (2 x slots x 256 x 2304; bench.py derives the live-row rate from the counts).
+  void gathered_value(int l, const int* rows, const int* counts, float* vrows, const float* cross, int B, int HB,
+                      int WB, int MR) {
     const int d = 256;
     ConvArgs a = conv_args(dl[l].vproj, cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, B, HB, WB, vrows,
                            (int64_t)MR * d, d, 0, true, nullptr, 0, 0, 0);
@@ -563,7 +570,16 @@ class Model {
     a.Wo = 1;
     a.rowmap = rows;
     a.rowmap_nimg = B;
+    if (value_compact && counts) {
+      a.rowcount = counts;
+      a.rowcap = MR / B;
+    }
     const double fl = 2.0 * MR * (double)d * 9 * dl[l].vproj.cin_real;
+    struct ClassScope {
+      const char*& c;
+      ClassScope(const char*& cc, const char* v) : c(cc) { c = v; }
+      ~ClassScope() { c = nullptr; }
+    } cls(force_class, "value_proj");
     launch("conv_x3", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
 
@@ -579,6 +595,7 @@ class Model {
     auto sfx = [](int s, int l) { return "_s" + std::to_string(s) + "l" + std::to_string(l); };
     auto rows_of = [&](int s, int l) { return reinterpret_cast<int*>(buf("value_taps" + sfx(s, l), (size_t)MR)); };
     auto slots_of = [&](int s, int l) { return reinterpret_cast<int*>(buf("value_slots" + sfx(s, l), (size_t)MR)); };
+    auto counts_of = [&](int s, int l) { return reinterpret_cast<int*>(buf("value_cnt" + sfx(s, l), (size_t)B)); };
     float* imgx = buf("ddim_img", (size_t)R * P * 2);
     float* tfe = buf("traj_feature", (size_t)R * d);
     float* pts = buf("pts", (size_t)R * P * 2);
@@ -595,6 +612,7 @@ class Model {
       ia.imgx = imgx;
       ia.rows = rows_of(0, 0);
       ia.slots = slots_of(0, 0);
+      ia.counts = counts_of(0, 0);
       ia.sa = vanilla ? 0.0f : std::sqrt(a8);
       ia.s1a = vanilla ? 1.0f : std::sqrt(1.0f - a8);
       ia.B = B;
@@ -616,7 +634,7 @@ class Model {
       for (int l = 0; l < 2; ++l) {
         const std::string sf = sfx(si, l);
         float* vrows = buf("value_rows" + sf, (size_t)MR * d);
-        gathered_value(l, rows_of(si, l), vrows, cross, B, HB, WB, MR);
+        gathered_value(l, rows_of(si, l), counts_of(si, l), vrows, cross, B, HB, WB, MR);
         if (tf_pending) {
           join();  // tf decoder: agent K / V and ego rows of both layers
           tf_pending = false;
@@ -641,9 +659,11 @@ class Model {
         if (l == 0) {
           m.next_rows = rows_of(si, 1);
           m.next_slots = slots_of(si, 1);
+          m.next_counts = counts_of(si, 1);
         } else if (si + 1 < steps) {
           m.next_rows = rows_of(si + 1, 0);
           m.next_slots = slots_of(si + 1, 0);
+          m.next_counts = counts_of(si + 1, 0);
           const int k = roll[si];
           const float a_t = ac[k], a_p = (k - ratio >= 0) ? ac[k - ratio] : 1.0f;
           m.ddim = 1;
@@ -747,8 +767,9 @@ class Model {
     DD_HIP_CHECK(hipEventRecord(a, st));
     f();
     DD_HIP_CHECK(hipEventRecord(b, st));
-    // conv / GEMM launches are attributed to the kernel the dispatcher actually chose
-    if (shape) name = last_conv_kernel();
+    // conv / GEMM launches are attributed to the kernel the dispatcher actually chose (or a forced class)
+    if (force_class) name = force_class;
+    else if (shape) name = last_conv_kernel();
     std::string detail;
     if (shape) {
       const ConvArgs& c = *shape;

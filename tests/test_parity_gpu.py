@@ -242,7 +242,8 @@ def test_bf16_resnet50_batch64_config_c4():
 
 def test_gathered_value_rows_match_dense_map(gpu_model):
     """f16x3 evaluates value_proj (blocks.py:68-76,114) only at the map pixels grid_sample's bilinear
-    taps read (blocks.py:101-122), each distinct pixel of a scene once (conv_x3 gathered rows):
+    taps read (blocks.py:101-122), each distinct pixel of a scene once (conv_x3 gathered rows, the scenes'
+    rows compacted into full tiles by their counts):
     the tap geometry must follow align_corners=False / zero padding, each scene's row list must be
     exactly its distinct tap pixels in pixel order (-1 past the count), every tap's slot must hold
     its pixel (-1 for zero-padded taps), and every gathered row must equal the fp32 dense map at its
@@ -265,6 +266,7 @@ def test_gathered_value_rows_match_dense_map(gpu_model):
         n = B * cap
         rows = gpu_model.tap("value_taps_s1l0")[:n].view(torch.int32).cpu().numpy()
         slots = gpu_model.tap("value_slots_s1l0")[:n].view(torch.int32).cpu().numpy()
+        counts = gpu_model.tap("value_cnt_s1l0")[:B].view(torch.int32).cpu().numpy()
         vals = gpu_model.tap("value_rows_s1l0", (n, 256)).double().cpu().numpy()
         pts = gpu_model.tap("pts", (B * Q * P, 2)).double().cpu().numpy()
     finally:
@@ -287,6 +289,7 @@ def test_gathered_value_rows_match_dense_map(gpu_model):
         uniq = np.unique(tp[tp >= 0])
         rs = rows[s_ * cap:(s_ + 1) * cap]
         assert np.array_equal(rs[:len(uniq)], uniq) and (rs[len(uniq):] == -1).all(), s_
+        assert counts[s_] == len(uniq), (s_, counts[s_], len(uniq))  # the compacted launch's row counts
     assert np.array_equal(slots < 0, pix < 0)
     live = slots >= 0
     assert np.array_equal(rows[slots[live]], pix[live])
@@ -419,3 +422,34 @@ def test_fused_token_pooling_matches_avgpool(gpu_model, seeded_sd, monkeypatch):
     for k, v in taps.items():
         assert float(np.abs(m.tap(k).cpu().numpy()[: v.size] - v).max()) <= 1e-6, k
     assert waypoint_l2(out, ref["trajectory"].numpy()) <= 1e-6
+
+
+def test_compacted_value_rows_equal_per_scene_tiles(gpu_model, seeded_sd, monkeypatch):
+    """The gathered value_proj with the scenes' rows compacted into full 128-row tiles (default) against one tile
+    run per scene (DDMI_VALUE_COMPACT=0): every output row is the same dot products in the same K order wherever
+    its tile sits, so every live row and the trajectory are bit-identical."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 6
+    inp = synthetic_inputs(B, 43)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"])
+    gpu_model.set_gemm_mode("f16x3")
+    try:
+        out = gpu_model.forward(feats, noise=nz)["trajectory"].numpy()
+        got = {f"s{s}l{l}": (gpu_model.tap(f"value_taps_s{s}l{l}").view(torch.int32).cpu().numpy()[: B * 640],
+                             gpu_model.tap(f"value_rows_s{s}l{l}").cpu().numpy()[: B * 640 * 256].reshape(-1, 256))
+               for s in range(2) for l in range(2)}
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    monkeypatch.setenv("DDMI_VALUE_COMPACT", "0")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+    ref = m.forward(feats, noise=nz)["trajectory"].numpy()
+    for k, (rows, vals) in got.items():
+        live = rows >= 0
+        r_rows = m.tap(f"value_taps_{k}").view(torch.int32).cpu().numpy()[: B * 640]
+        r_vals = m.tap(f"value_rows_{k}").cpu().numpy()[: B * 640 * 256].reshape(-1, 256)
+        assert np.array_equal(rows, r_rows), k
+        assert np.array_equal(vals[live], r_vals[live]), k
+    m.close()
+    assert np.array_equal(out, ref)
