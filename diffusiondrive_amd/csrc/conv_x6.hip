@@ -150,7 +150,7 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
 __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
-                                                               int ntn, int nchunks) {
+                                                               int ntn, int nchunks, int diag) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = TH * TW;
   constexpr int TM = BM / WM / 32;
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   const int nq = n0 + 4 * qn;
   const bool nv = nq < a.Cout;
   float* out = a.out + (int64_t)nimg * a.out_sn + nq;
-  const float* res = a.res ? a.res + (int64_t)nimg * a.res_sn + nq : nullptr;
+  const float* res = (a.res && !(diag & 1)) ? a.res + (int64_t)nimg * a.res_sn + nq : nullptr;
   const int osh = (int)a.out_sh, osw = (int)a.out_sw;
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
   // the residual / scale / bias loads go out before the accumulators are parked, so their latency
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
       v.z = fmaxf(v.z, 0.f);
       v.w = fmaxf(v.w, 0.f);
     }
-    *reinterpret_cast<x6f4*>(out + ooff[k]) = v;
+    if (!(diag & 2)) *reinterpret_cast<x6f4*>(out + ooff[k]) = v;
     if (a.pool_out) *reinterpret_cast<x6f4*>(ct + p * BN + 4 * qn) = v;  // the finished value, for the pool
   }
   if (a.pool_out) {
@@ -563,8 +563,12 @@ static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
                                   std::to_string(BN) + "," + std::to_string(WM) + "," + std::to_string(WN) +
                                   (PREC ? ",bf16>" : ">");
   set_last_conv_config(name.c_str());
+  // timing diagnostic, read per dispatch (graph replays do not dispatch): DDMI_X6_DIAG bit 0 = skip the residual
+  // read, bit 1 = skip the output store (WRONG results; tools/gpu_x6exp.sh)
+  const char* de = getenv("DDMI_X6_DIAG");
+  const int diag = de ? atoi(de) : 0;
   hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0,
-                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32));
+                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
   DD_HIP_CHECK(hipGetLastError());
 }
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
