@@ -121,6 +121,37 @@ __device__ inline void epi_row_table(const ConvArgs& a, int m0, int M, int tid, 
   }
 }
 
+// Exclusive prefix of n <= 256 per-image row counts into pre[0..n] (pre[n] = total), by the first wave of the
+// workgroup: 4 counts per lane, a 64-lane shuffle scan (a serial loop by one thread cost ~4 us per workgroup).
+// Every thread must call it; it ends with a workgroup barrier.
+__device__ inline void rowcount_prefix(const int* counts, int n, int* pre) {
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    int c[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * tid + j;
+      c[j] = i < n ? counts[i] : 0;
+      s += c[j];
+    }
+    int inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (tid >= o) inc += v;
+    }
+    int run = inc - s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * tid + j;
+      if (i <= n) pre[i] = run;
+      run += c[j];
+    }
+    if (tid == 63 && n == 256) pre[256] = run;
+  }
+  __syncthreads();
+}
+
 // Can epi_quads serve this launch? Every output / residual row starts 16-B aligned and Cout % 4 == 0.
 __device__ inline bool epi_quads_ok(const ConvArgs& a) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -219,6 +250,31 @@ void set_last_conv_pooled(bool p);
 // "conv_x6<8,32,128,4,2>" (TH, TW, BN, wave grid), "conv_x5<256,256>", "conv_x3<128,128,f16x3>"
 const char* last_conv_config();
 void set_last_conv_config(const char* cfg);
+
+// ----------------------------------------------------------------------------------------
+// The gathered value_proj (value_proj.hip): value rows = ReLU(conv3x3(map) + bias) at the scenes' distinct tap
+// pixels, rows[b * cap + l] (l < counts[b]) = pixel b * 4096 + y * 64 + x of the (B, 64, 64, 256) NHWC map; row
+// b * cap + l of `out` receives it. wh / wl: the f16x3 weight images [256][ldh] (K order kh, kw, ci) with
+// per-column inverse scales wsinv; part: [3][B * cap][256] fp32 scratch; tile_cnt: vproj_tiles(B, cap) zeroed
+// words (left zeroed by every launch).
+struct VprojArgs {
+  const float* map = nullptr;
+  const uint16_t* wh = nullptr;
+  const uint16_t* wl = nullptr;
+  const float* wsinv = nullptr;
+  int ldh = 0;
+  const float* bias = nullptr;
+  const int* rows = nullptr;
+  const int* counts = nullptr;
+  int B = 0, cap = 0;
+  float* part = nullptr;
+  unsigned* tile_cnt = nullptr;
+  float* out = nullptr;
+  unsigned* flags = nullptr;
+};
+bool vproj_supported(int C, int Cout, int H, int W);
+size_t vproj_tiles(int B, int cap);
+void launch_vproj(const VprojArgs& a, hipStream_t st);
 
 // ----------------------------------------------------------------------------------------
 // Bandwidth / small kernels (elementwise.hip)

@@ -102,17 +102,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     if (a.rowcount) {
       // exclusive prefix of the images' live-row counts; launch row m = the m-th live row in image order
       const int nimg = a.rowmap_nimg;
-      for (int n = tid; n < nimg; n += NT) g_pre[n + 1] = a.rowcount[n];
-      __syncthreads();
-      if (tid == 0) {
-        int s = 0;
-        g_pre[0] = 0;
-        for (int n = 1; n <= nimg; ++n) {
-          s += g_pre[n];
-          g_pre[n] = s;
-        }
-      }
-      __syncthreads();
+      rowcount_prefix(a.rowcount, nimg, g_pre);
       const int total = g_pre[nimg];
       if (m0 >= total) return;  // past every live row (workgroup-uniform)
       for (int r = tid; r < BM; r += NT) {

@@ -149,6 +149,7 @@ class Model {
   bool value_gather = true;
   bool value_dedup = true;
   bool value_compact = true;         // DDMI_VALUE_COMPACT=0: gathered value rows in per-scene tile runs
+  bool value_splitk = true;          // DDMI_VALUE_SPLITK=0: the gathered value_proj on conv_x3 (one launch, K whole)
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
   // bev_proj (DDMI_BEVPROJ): 2 "fused" = one bevproj.hip pass (f16x3 / bf16 modes; fp32 mode uses 1),
   // 1 "lowres" = keyval half at 8 x 8, upsample, K = 64 GEMM, LayerNorm; 0 "concat" = concat at 64 x 64
@@ -222,6 +223,7 @@ class Model {
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_COMPACT")) value_compact = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VALUE_SPLITK")) value_splitk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BEVPROJ")) {
       if (!strcmp(e, "fused")) bevproj_mode = 2;
       else if (!strcmp(e, "lowres")) bevproj_mode = 1;
@@ -575,6 +577,27 @@ class Model {
       a.rowcap = MR / B;
     }
     const double fl = 2.0 * MR * (double)d * 9 * dl[l].vproj.cin_real;
+    const Conv& vc = dl[l].vproj;
+    if (value_splitk && counts && vproj_supported(vc.cin, vc.cout, HB, WB) && a.wh && a.prec == 0) {
+      // the split-K kernel (value_proj.hip): compacted rows, K split by filter row, deterministic combine
+      VprojArgs v;
+      v.map = cross;
+      v.wh = a.wh;
+      v.wl = a.wl;
+      v.wsinv = a.wsinv;
+      v.ldh = (int)a.ldh;
+      v.bias = a.bias;
+      v.rows = rows;
+      v.counts = counts;
+      v.B = B;
+      v.cap = MR / B;
+      v.part = buf("vproj_part", (size_t)3 * MR * d);
+      v.tile_cnt = reinterpret_cast<unsigned*>(buf_zeroed("vproj_cnt", vproj_tiles(B, MR / B)));
+      v.out = vrows;
+      v.flags = num_flags;
+      launch("value_proj", fl, [&] { launch_vproj(v, st); });
+      return;
+    }
     struct ClassScope {
       const char*& c;
       ClassScope(const char*& cc, const char* v) : c(cc) { c = v; }
@@ -694,6 +717,15 @@ class Model {
 
   // ------------------------------------------------------------------ runtime helpers
   const float* W(size_t off) const { return ar.ptr(off); }
+
+  // a workspace buffer whose words start zeroed when it is (re)allocated (allocation only happens in eager,
+  // uncaptured forwards; kernels that use such words leave them zeroed)
+  float* buf_zeroed(const std::string& name, size_t n) {
+    const uint64_t g = generation;
+    float* p = buf(name, n);
+    if (generation != g) DD_HIP_CHECK(hipMemset(p, 0, std::max<size_t>(n, 4) * sizeof(float)));
+    return p;
+  }
 
   float* buf(const std::string& name, size_t n) {
     auto it = bufs.find(name);
@@ -1100,9 +1132,13 @@ class Model {
     ln(g.lnf, X, C, Hb, C, M);  // Hb = ln_f(x): image tokens rows 0..255, lidar 256..319 per scene
     conv(i2l[i], Hb + (size_t)nimg * C, (int64_t)T * C, (int64_t)8 * C, C, B, 8, 8, LO, (int64_t)64 * Cl,
          (int64_t)8 * Cl, Cl, false);
-    View4 gi{Hb, (int64_t)T * C, (int64_t)32 * C, C, 1};
-    View4 io{imgf, (int64_t)Hi * Wi * C, (int64_t)Wi * C, C, 1};
-    launch("bilinear", 0, [&] { launch_bilinear(gi, B, 8, 32, C, io, Hi, Wi, 8.0f / Hi, 32.0f / Wi, 1, st); });
+    // the image branch after the last fusion is never read (the BEV path takes the LiDAR features:
+    // transformer_decoder_join, transfuser_backbone.py:204-205), so its upsample-add is skipped at i == 3
+    if (i + 1 < 4) {
+      View4 gi{Hb, (int64_t)T * C, (int64_t)32 * C, C, 1};
+      View4 io{imgf, (int64_t)Hi * Wi * C, (int64_t)Wi * C, C, 1};
+      launch("bilinear", 0, [&] { launch_bilinear(gi, B, 8, 32, C, io, Hi, Wi, 8.0f / Hi, 32.0f / Wi, 1, st); });
+    }
     View4 gl{LO, (int64_t)64 * Cl, (int64_t)8 * Cl, Cl, 1};
     View4 lo{lidf, (int64_t)Hl * Wl * Cl, (int64_t)Wl * Cl, Cl, 1};
     launch("bilinear", 0, [&] { launch_bilinear(gl, B, 8, 8, Cl, lo, Hl, Wl, 8.0f / Hl, 8.0f / Wl, 1, st); });
@@ -1211,7 +1247,7 @@ class Model {
       join();
       fuse(s, xi, B, Hi, Wi, xl, Hl, Wl, ipooled, lpooled);
     }
-    alias("img_l4", xi);
+    alias("img_l4", xi);  // before the (skipped, dead) last fusion add
     alias("bev_feature", xl);  // (B, 8, 8, 512) NHWC; transformer_decoder_join -> fused = lidar (:204-205)
     // everything past the backbone runs in the head arithmetic (bf16 mode: f16x3; see head_mode)
     ModeScope head_scope(this, head_mode());
