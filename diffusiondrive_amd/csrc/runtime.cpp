@@ -149,7 +149,6 @@ class Model {
   bool value_gather = true;
   bool value_dedup = true;
   bool value_compact = true;         // DDMI_VALUE_COMPACT=0: gathered value rows in per-scene tile runs
-  bool value_splitk = true;          // DDMI_VALUE_SPLITK=0: the gathered value_proj on conv_x3 (one launch, K whole)
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
   // bev_proj (DDMI_BEVPROJ): 2 "fused" = one bevproj.hip pass (f16x3 / bf16 modes; fp32 mode uses 1),
   // 1 "lowres" = keyval half at 8 x 8, upsample, K = 64 GEMM, LayerNorm; 0 "concat" = concat at 64 x 64
@@ -223,7 +222,6 @@ class Model {
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_COMPACT")) value_compact = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_VALUE_SPLITK")) value_splitk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BEVPROJ")) {
       if (!strcmp(e, "fused")) bevproj_mode = 2;
       else if (!strcmp(e, "lowres")) bevproj_mode = 1;
@@ -577,27 +575,6 @@ class Model {
       a.rowcap = MR / B;
     }
     const double fl = 2.0 * MR * (double)d * 9 * dl[l].vproj.cin_real;
-    const Conv& vc = dl[l].vproj;
-    if (value_splitk && counts && vproj_supported(vc.cin, vc.cout, HB, WB) && a.wh && a.prec == 0) {
-      // the split-K kernel (value_proj.hip): compacted rows, K split by filter row, deterministic combine
-      VprojArgs v;
-      v.map = cross;
-      v.wh = a.wh;
-      v.wl = a.wl;
-      v.wsinv = a.wsinv;
-      v.ldh = (int)a.ldh;
-      v.bias = a.bias;
-      v.rows = rows;
-      v.counts = counts;
-      v.B = B;
-      v.cap = MR / B;
-      v.part = buf("vproj_part", (size_t)3 * MR * d);
-      v.tile_cnt = reinterpret_cast<unsigned*>(buf_zeroed("vproj_cnt", vproj_tiles(B, MR / B)));
-      v.out = vrows;
-      v.flags = num_flags;
-      launch("value_proj", fl, [&] { launch_vproj(v, st); });
-      return;
-    }
     struct ClassScope {
       const char*& c;
       ClassScope(const char*& cc, const char* v) : c(cc) { c = v; }
@@ -717,15 +694,6 @@ class Model {
 
   // ------------------------------------------------------------------ runtime helpers
   const float* W(size_t off) const { return ar.ptr(off); }
-
-  // a workspace buffer whose words start zeroed when it is (re)allocated (allocation only happens in eager,
-  // uncaptured forwards; kernels that use such words leave them zeroed)
-  float* buf_zeroed(const std::string& name, size_t n) {
-    const uint64_t g = generation;
-    float* p = buf(name, n);
-    if (generation != g) DD_HIP_CHECK(hipMemset(p, 0, std::max<size_t>(n, 4) * sizeof(float)));
-    return p;
-  }
 
   float* buf(const std::string& name, size_t n) {
     auto it = bufs.find(name);
