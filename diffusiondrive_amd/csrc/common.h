@@ -240,7 +240,12 @@ void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
 void launch_conv_x3(const ConvArgs& a, hipStream_t st);
 // Fused stem conv 7x7/2 (Cin 4, Cout 64, f16x3) + bias + ReLU + maxpool 3x3/2 into pool_out (B,Hp,Wp,64)
 // (stem_pool.hip); false when `a` is not such a stem (then nothing is launched).
-bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStream_t st);
+// src (optional): the device word holding the address of the reference's NCHW input of src_c channels (read by the
+// kernel; the NHWC4 a.in is then unused).
+bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStream_t st,
+                      const float* const* src = nullptr, int src_c = 0);
+// Device-side input table: tab[0] = a, tab[1] = b (one thread; launched per forward outside the captured graph).
+void launch_set_ptrs(const float** tab, const float* a, const float* b, hipStream_t st);
 // name of the kernel the last conv / GEMM dispatch on this thread went to ("conv_gemm", "conv_x3",
 // "conv_x5", "conv_x6"); the runtime's profiler attributes launch time per kernel with it
 const char* last_conv_kernel();

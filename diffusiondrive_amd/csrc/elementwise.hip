@@ -33,6 +33,18 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, float* __restr
   }
 }
 
+__global__ void set_ptrs_kernel(const float** tab, const float* a, const float* b) {
+  if (threadIdx.x == 0) {
+    tab[0] = a;
+    tab[1] = b;
+  }
+}
+
+void launch_set_ptrs(const float** tab, const float* a, const float* b, hipStream_t st) {
+  hipLaunchKernelGGL(set_ptrs_kernel, dim3(1), dim3(64), 0, st, tab, a, b);
+  DD_HIP_CHECK(hipGetLastError());
+}
+
 void launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int H, int W, int Cp, hipStream_t st) {
   if (C > 8 || Cp < C) throw std::runtime_error("nchw_to_nhwc: unsupported channel count");
   const int64_t n = (int64_t)B * H * W;

@@ -149,6 +149,8 @@ class Model {
   bool value_gather = true;
   bool value_dedup = true;
   bool value_compact = true;         // DDMI_VALUE_COMPACT=0: gathered value rows in per-scene tile runs
+  bool stem_nchw = true;             // see use_nchw_stem
+  const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
   // bev_proj (DDMI_BEVPROJ): 2 "fused" = one bevproj.hip pass (f16x3 / bf16 modes; fp32 mode uses 1),
   // 1 "lowres" = keyval half at 8 x 8, upsample, K = 64 GEMM, LayerNorm; 0 "concat" = concat at 64 x 64
@@ -222,6 +224,9 @@ class Model {
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_COMPACT")) value_compact = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
+    DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
+    DD_HIP_CHECK(hipMemset(in_tab, 0, 4 * sizeof(float*)));
     if (const char* e = getenv("DDMI_BEVPROJ")) {
       if (!strcmp(e, "fused")) bevproj_mode = 2;
       else if (!strcmp(e, "lowres")) bevproj_mode = 1;
@@ -278,6 +283,7 @@ class Model {
     if (st_main) (void)hipStreamDestroy(st_main);
     if (st_side) (void)hipStreamDestroy(st_side);
     if (num_flags) (void)hipFree(num_flags);
+    if (in_tab) (void)hipFree(in_tab);
     if (tf_mk_layers) (void)hipFree(tf_mk_layers);
     for (auto& kv : bufs) (void)hipFree(kv.second.first);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
@@ -881,14 +887,21 @@ class Model {
   }
   // timm stem conv1 / bn1 / act1 + maxpool 3x3/2: one fused kernel (stem_pool.hip) in f16x3 mode,
   // otherwise the conv into `stem` and the pool from it
-  void stem_and_pool(const Conv& c, const float* in4, int N, int H, int Wd, float* stem, float* pool, int hp, int wp) {
+  // in_idx / in_c: with the NCHW stem (use_nchw_stem) the kernel reads the caller's NCHW input of in_c channels
+  // through the device input table entry in_idx instead of the NHWC4 copy (which is then never made)
+  void stem_and_pool(const Conv& c, const float* in4, int N, int H, int Wd, float* stem, float* pool, int hp, int wp,
+                     int in_idx, int in_c) {
     const int hs = (H + 2 * c.pad - c.k) / c.stride + 1, ws = (Wd + 2 * c.pad - c.k) / c.stride + 1;
     ConvArgs a = conv_args(c, in4, (int64_t)H * Wd * c.cin, (int64_t)Wd * c.cin, c.cin, N, H, Wd, stem,
                            (int64_t)hs * ws * c.cout, (int64_t)ws * c.cout, c.cout, true, nullptr, 0, 0, 0);
     bool done = false;
     const double fl = 2.0 * N * hs * ws * (double)c.cout * c.k * c.k * c.cin_real;
-    launch("stem_pool", fl, [&] { done = launch_stem_pool(a, pool, hp, wp, st); });
+    const bool nchw = use_nchw_stem();
+    launch("stem_pool", fl, [&] {
+      done = launch_stem_pool(a, pool, hp, wp, st, nchw ? in_tab + in_idx : nullptr, nchw ? in_c : 0);
+    });
     if (done) return;
+    if (nchw) throw std::runtime_error("stem: the NCHW-input fused stem refused this shape (DDMI_STEM_NCHW=0 avoids it)");
     conv_c(c, in4, N, H, Wd, stem, true);
     launch("pool", 0, [&] { launch_maxpool3x3s2(stem, pool, N, hs, ws, c.cout, hp, wp, st); });
   }
@@ -1118,6 +1131,9 @@ class Model {
   // FPN, BEV tokens, tf decoder, bev_proj, the optional heads and the trajectory head with its time MLP - runs
   // in f16x3 (on the megakernels), so the decoder adds fp32-class rounding only to the backbone's bf16 error.
   int head_mode() const { return gemm_mode == DD_GEMM_BF16 ? DD_GEMM_F16X3 : gemm_mode; }
+  // the fused stems (f16x3 / bf16) read the caller's NCHW camera / LiDAR tensors directly (DDMI_STEM_NCHW=0: the
+  // NHWC4 transpose pass first, as the fp32 mode always does)
+  bool use_nchw_stem() const { return stem_nchw && gemm_mode != DD_GEMM_FP32 && cfg.lidar_channels <= 3; }
   struct ModeScope {
     Model* m;
     int saved;
@@ -1182,8 +1198,9 @@ class Model {
   void forward_body(int B, int steps, bool heads) {
     const int d = 256, Q = cfg.num_modes, P = cfg.num_poses;
     const int HC = cfg.cam_h, WC = cfg.cam_w, HL = cfg.lidar_h, WL = cfg.lidar_w;
-    float* cam4 = bufs["in_cam4"].first;
-    float* lid4 = bufs["in_lid4"].first;
+    const bool nchw = use_nchw_stem();
+    float* cam4 = nchw ? nullptr : bufs.at("in_cam4").first;
+    float* lid4 = nchw ? nullptr : bufs.at("in_lid4").first;
     const float* stat = bufs["in_status"].first;
     const float* noise = bufs["in_noise"].first;
 
@@ -1198,8 +1215,8 @@ class Model {
     const int hl2 = (hl + 2 - 3) / 2 + 1, wl2 = (wl + 2 - 3) / 2 + 1;
     float* pool_l = buf("lid_pool", (size_t)B * hl2 * wl2 * 64);
     fork();
-    side([&] { stem_and_pool(lid.stem, lid4, B, HL, WL, stem_l, pool_l, hl2, wl2); });
-    stem_and_pool(img.stem, cam4, B, HC, WC, stem_i, pool_i, hi2, wi2);
+    side([&] { stem_and_pool(lid.stem, lid4, B, HL, WL, stem_l, pool_l, hl2, wl2, 1, cfg.lidar_channels); });
+    stem_and_pool(img.stem, cam4, B, HC, WC, stem_i, pool_i, hi2, wi2, 0, 3);
 
     // ---- 4 scales: trunk stages (image on the main stream, LiDAR beside it) + GPT fusion
     float* xi = pool_i;
@@ -1590,13 +1607,19 @@ class Model {
   // noise == NULL: draw it on the device for scenes [scene0, scene0 + B) of the handle's stream
   void stage_inputs(const float* camera, const float* lidar, const float* status, const float* noise, int B,
                     uint64_t scene0) {
-    float* cam4 = buf("in_cam4", (size_t)B * cfg.cam_h * cfg.cam_w * 4);
-    float* lid4 = buf("in_lid4", (size_t)B * cfg.lidar_h * cfg.lidar_w * 4);
     float* st_in = buf("in_status", (size_t)B * 8);
     const size_t per = (size_t)cfg.num_modes * cfg.num_poses * 2;
     float* nz = buf("in_noise", (size_t)B * per);
-    launch("misc", 0, [&] { launch_nchw_to_nhwc(camera, cam4, B, 3, cfg.cam_h, cfg.cam_w, 4, st); });
-    launch("misc", 0, [&] { launch_nchw_to_nhwc(lidar, lid4, B, cfg.lidar_channels, cfg.lidar_h, cfg.lidar_w, 4, st); });
+    if (use_nchw_stem()) {
+      // the stems read the caller's NCHW tensors in place: only their addresses go to the device table (the
+      // captured graph reads them from there); the caller's buffers outlive the forward (stream order)
+      launch("misc", 0, [&] { launch_set_ptrs(in_tab, camera, lidar, st); });
+    } else {
+      float* cam4 = buf("in_cam4", (size_t)B * cfg.cam_h * cfg.cam_w * 4);
+      float* lid4 = buf("in_lid4", (size_t)B * cfg.lidar_h * cfg.lidar_w * 4);
+      launch("misc", 0, [&] { launch_nchw_to_nhwc(camera, cam4, B, 3, cfg.cam_h, cfg.cam_w, 4, st); });
+      launch("misc", 0, [&] { launch_nchw_to_nhwc(lidar, lid4, B, cfg.lidar_channels, cfg.lidar_h, cfg.lidar_w, 4, st); });
+    }
     DD_HIP_CHECK(hipMemcpyAsync(st_in, status, sizeof(float) * B * 8, hipMemcpyDeviceToDevice, st));
     if (noise)
       DD_HIP_CHECK(hipMemcpyAsync(nz, noise, sizeof(float) * B * per, hipMemcpyDeviceToDevice, st));

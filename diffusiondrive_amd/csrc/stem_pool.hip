@@ -28,6 +28,8 @@
 //    loaded into registers while the current tile's MFMAs run.
 // Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.17 x recompute,
 // 224 / 196 K padding; HBM traffic = the input once (+ halo re-reads) + the pooled map.
+#include <type_traits>
+
 #include "common.h"
 
 namespace ddmi {
@@ -76,8 +78,12 @@ __device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
   lo = __builtin_convertvector(r, sp_h4);
 }
 
-template <int PREC>
-__global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__ in, int H, int W, int Hs, int Ws,
+// SRC_C = 0: the input is the NHWC image padded to 4 channels at `in`; SRC_C = 1..3: the reference's NCHW feature
+// tensor with SRC_C channels, whose address the kernel reads from *src (a device word the runtime sets per call
+// outside the captured graph), the missing channels zero - the same 4-channel pixels, without the transpose pass.
+template <int PREC, int SRC_C>
+__global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__ in, const float* const* src, int H,
+                                                       int W, int Hs, int Ws,
                                                        int Hp, int Wp, const uint16_t* __restrict__ wh,
                                                        const uint16_t* __restrict__ wl, int ldh,
                                                        const float* __restrict__ wsinv,
@@ -121,6 +127,8 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     b = t2 / tiles_y;
   };
   sp_f4 pre[ILD];
+  const float* __restrict__ img = SRC_C ? *src : in;
+  const int64_t plane = (int64_t)H * W;
   auto load_patch = [&](int t) {
     int b, py0, px0;
     tile_origin(t, b, py0, px0);
@@ -131,8 +139,20 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       const int r = e / IW, c = e - (e / IW) * IW;
       const int iy = iy0 + r, ix = ix0 + c;
       const bool ok = e < IH * IW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      pre[i] = ok ? *reinterpret_cast<const sp_f4*>(in + (((int64_t)b * H + iy) * W + ix) * 4)
-                  : (sp_f4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (SRC_C == 0) {
+        pre[i] = ok ? *reinterpret_cast<const sp_f4*>(img + (((int64_t)b * H + iy) * W + ix) * 4)
+                    : (sp_f4){0.f, 0.f, 0.f, 0.f};
+      } else {
+        // consecutive threads take consecutive columns: each plane's loads coalesce
+        const float* p = img + (int64_t)b * SRC_C * plane + (int64_t)iy * W + ix;
+        sp_f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (ok) {
+          v.x = p[0];
+          if constexpr (SRC_C > 1) v.y = p[plane];
+          if constexpr (SRC_C > 2) v.z = p[2 * plane];
+        }
+        pre[i] = v;
+      }
     }
   };
   auto store_patch = [&]() {
@@ -225,17 +245,23 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
 }  // namespace
 
 // Returns false when the conv is not a 7x7 / s2 / p3, Cin 4, Cout 64 f16x3 / bf16 stem on a contiguous
-// NHWC4 input (the caller then runs the conv and the pool separately).
-bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStream_t st) {
+// NHWC4 input (src == nullptr) or on the NCHW tensor of src_c channels whose address is the device word *src
+// (the caller then runs the conv and the pool separately).
+bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStream_t st, const float* const* src,
+                      int src_c) {
   if (!a.wh || (a.prec == 0 && !a.wl) || (a.prec != 0 && a.prec != 1) || !a.wsinv) return false;
   if (a.KH != 7 || a.KW != 7 || a.stride != 2 || a.pad != 3 || a.Cin != 4 || a.Cout != 64 || a.batch != 1 || a.res ||
       !a.relu)
     return false;
-  if (a.in_sw != 4 || a.in_sh != (int64_t)a.W * 4 || a.in_sn != (int64_t)a.H * a.W * 4 || a.ldh < 196 || a.ldh % 4)
+  if (src) {
+    if (src_c < 1 || src_c > 3 || (int64_t)a.Nimg * src_c * a.H * a.W >= (int64_t(1) << 31)) return false;
+  } else if (a.in_sw != 4 || a.in_sh != (int64_t)a.W * 4 || a.in_sn != (int64_t)a.H * a.W * 4) {
     return false;
+  }
+  if (a.ldh < 196 || a.ldh % 4) return false;
   const int Hs = a.Ho, Ws = a.Wo;
   if (Hp != (Hs + 2 - 3) / 2 + 1 || Wp != (Ws + 2 - 3) / 2 + 1) return false;
-  if ((reinterpret_cast<uintptr_t>(a.in) & 15) || (reinterpret_cast<uintptr_t>(pool_out) & 15) ||
+  if ((!src && (reinterpret_cast<uintptr_t>(a.in) & 15)) || (reinterpret_cast<uintptr_t>(pool_out) & 15) ||
       (reinterpret_cast<uintptr_t>(a.wh) & 7) || (a.prec == 0 && (reinterpret_cast<uintptr_t>(a.wl) & 7)))
     return false;
   const int tiles_x = (Wp + PW - 1) / PW, tiles_y = (Hp + PH - 1) / PH;
@@ -247,16 +273,26 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int per_cu = NT == 512 ? 1 : 2;
   const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
-  static std::atomic<uint64_t> attr[2];
-  auto go = [&](auto kern) {
-    set_max_lds_once(attr[a.prec], reinterpret_cast<const void*>(kern), LDS_BYTES);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
+  static std::atomic<uint64_t> attr[2][4];
+  auto go = [&](auto kern, int c) {
+    set_max_lds_once(attr[a.prec][c], reinterpret_cast<const void*>(kern), LDS_BYTES);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, src, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
                        (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
   };
+  const int c = src ? src_c : 0;
+  auto pick = [&](auto PR) {
+    constexpr int P = decltype(PR)::value;
+    switch (c) {
+      case 1: go(stem_pool_kernel<P, 1>, 1); break;
+      case 2: go(stem_pool_kernel<P, 2>, 2); break;
+      case 3: go(stem_pool_kernel<P, 3>, 3); break;
+      default: go(stem_pool_kernel<P, 0>, 0); break;
+    }
+  };
   if (a.prec == 1)
-    go(stem_pool_kernel<1>);
+    pick(std::integral_constant<int, 1>());
   else
-    go(stem_pool_kernel<0>);
+    pick(std::integral_constant<int, 0>());
   set_last_conv_config(a.prec == 1 ? "stem_pool<bf16>" : "stem_pool<f16x3>");
   DD_HIP_CHECK(hipGetLastError());
   return true;

@@ -458,3 +458,34 @@ def test_compacted_value_rows_equal_per_scene_tiles(gpu_model, seeded_sd, monkey
         assert np.array_equal(rows, ref[k][0]), k
         assert np.array_equal(vals[live], ref[k][1][live]), k
     assert np.array_equal(out, ref_out)
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "bf16"])
+def test_nchw_stem_equals_nhwc4_stem(gpu_model, seeded_sd, monkeypatch, mode):
+    """The fused stems read the caller's NCHW camera / LiDAR tensors in place (through the handle's device input
+    table) instead of an NHWC4 copy made by a transpose pass first (DDMI_STEM_NCHW=0): the same 4-channel pixels
+    reach the same arithmetic, so the pooled stem maps and the trajectory are bit-identical - also on a forward
+    whose inputs sit at new addresses (the captured graph reads the table, not a baked pointer)."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 3
+    inp = synthetic_inputs(B, 47)
+    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"]).cuda()
+    gpu_model.set_gemm_mode(mode)
+    try:
+        a = gpu_model.forward(feats, noise=nz)["trajectory"].cpu().numpy()
+        # replay (graph) with the same data at other device addresses
+        moved = {k: v.clone() for k, v in feats.items()}
+        b = gpu_model.forward(moved, noise=nz)["trajectory"].cpu().numpy()
+        pools = [gpu_model.tap(n).cpu().numpy() for n in ("img_pool", "lid_pool")]
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    monkeypatch.setenv("DDMI_STEM_NCHW", "0")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm=mode)
+    ref = m.forward(feats, noise=nz)["trajectory"].cpu().numpy()
+    ref_pools = [m.tap(n).cpu().numpy() for n in ("img_pool", "lid_pool")]
+    m.close()
+    assert np.array_equal(a, ref) and np.array_equal(b, ref)
+    for p, r in zip(pools, ref_pools):
+        assert np.array_equal(p[: r.size], r[: p.size])
