@@ -452,6 +452,8 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
     if (t == 2) { launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st); return true; }   // 256 x 256
     if (t == 3) { launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st); return true; }   // 256 x 64
     if (t == 4) { launch_x5_cfg<2, 2, 2, 2, 4>(a, M, K, st); return true; }   // 128 x 128, 4 waves
+    if (t == 5) { launch_x5_cfg<2, 4, 3, 2, 2>(a, M, K, st); return true; }   // 192 x 256, 8 waves
+    if (t == 6) { launch_x5_cfg<2, 2, 3, 2, 3>(a, M, K, st); return true; }   // 192 x 128, 4 waves
   }
   const int64_t m256 = (M + 255) / 256;
   const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;
@@ -460,6 +462,13 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   // 52 -> 43 us, MLP-up C = 128: 34 -> 31 us), 256 x 128 for Cout = 256 k + 128 (qkv C = 128: 25 -> 23 us);
   // Cout = 256 GEMMs with 80 tiles stay on conv_x3 (tools/micro/conv_bench, DDMI_X5_TILE)
   const bool gemm = a.KH * a.KW == 1 && a.stride == 1;
+  // short-K GEMMs with Cout = 512 / 1024 fill more of the chip with 192 x 256 tiles (proj C = 512: 61 -> 57 us,
+  // MLP-up C = 256: 72 -> 65 us, C = 128: 30 -> 27 us); K = 2048 and the qkv shapes lose with the 3 x 2 wave
+  // fragment layout (MLP-down 160 -> 162 us, qkv C = 512: 116 -> 145 us)
+  if (gemm && K <= 512 && (a.Cout == 512 || a.Cout == 1024) && M >= 16384) {
+    launch_x5_cfg<2, 4, 3, 2, 2>(a, M, K, st);  // 192 x 256, 8 waves
+    return true;
+  }
   if (a.Cout <= 64) {
     if (m256 < 256) return false;
     launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st);  // 256 x 64, 4 waves
