@@ -30,6 +30,13 @@
 // 59 -> 42 us, hs 16 / 32: -11 %; tools/micro/attn_bench.py, same box); 5 at hs = 128, whose 10-wave form spills
 #define DDMI_ATTN_NW 10
 #define DDMI_ATTN_NW128 5
+// score operand splits: 2 = f16x3's three products (default), 3 = six products on three-way splits. The two agree
+// to fp32 rounding (attention output vs a float64 reference: 4-10e-7 relative for both, tools/micro/attn_bench.py);
+// the three-way form spends 2x the score MFMAs, a third K image and 32 more registers (hs 128: 118 -> 81 us,
+// hs 64: 40 -> 34 us, same box, profiles/round3_i_attn_ss.txt). prec 2 (the bf16 backbone mode) keeps SS = 3: that
+// mode's C4 bar statistic (max over 1280 trajectories of the bf16 forward) sits at the edge of its 0.1 m bar and
+// moved 0.081 -> 0.105 m under this fp32-rounding-level change
+#define DDMI_ATTN_SS_DEFAULT 2
 #include "mk_core.h"
 
 namespace ddmi {
@@ -220,12 +227,12 @@ __global__ __launch_bounds__(256) void gpt_attn_kernel(const float* __restrict__
 // f16x3 form (the f16x3 / bf16 modes): NW waves per workgroup, one per 32-query block (T / 32 NW
 // workgroups per (scene, head); at T = 320 NW = 10 for hs <= 64, 5 for hs = 128, whose 10-wave form spills),
 // flash-style over 32-key
-// tiles staged in LDS already split (K three ways as key rows, V two ways transposed to dimension rows;
+// tiles staged in LDS already split (K two (SS = 3: three) ways as key rows, V two ways transposed to dimension rows;
 // double-buffered at hs <= 32, single at 64 / 128 so 2-3 workgroups share a CU), so no wave splits an
 // operand element more than once:
-//  * S^T = K Q^T on v_mfma_f32_32x32x16_f16 with both operands split three ways (6 products: the
-//    softmax turns score error into relative probability error) - keys on the accumulator rows,
-//    queries on the lanes, so each lane owns one query's online-softmax state (with lane ^ 32);
+//  * S^T = K Q^T on v_mfma_f32_32x32x16_f16 with both operands split two ways (f16x3's 3 products; SS = 3
+//    keeps the earlier six-product form on three-way splits for precision studies) - keys on the accumulator
+//    rows, queries on the lanes, so each lane owns one query's online-softmax state (with lane ^ 32);
 //  * O = P V with P taken straight from the S^T accumulators as the A operand: an MFMA step's k order
 //    is free, so it is the C layout's key order (lane half hh, element e <-> key 16 s + 4 hh + (e & 3)
 //    + 8 (e >> 2)), and V's B fragment gathers the same keys from the staged rows;
@@ -273,19 +280,20 @@ __device__ inline void split3x2(float a, float b, at_h2& hi, at_h2& mi, at_h2& l
 
 // LDS images per stage of 32 keys (halfs): K split three ways [3][32 keys][HS + 8] (16-B rows 4 banks apart),
 // V^T split two ways [2][HS dims][36] (8-B reads of 4 consecutive keys, 18-dword rows -> conflict-free)
-template <int HS>
+template <int HS, int SS>
 struct AttnLds {
   static constexpr int KPH = HS + 8;               // K image row pitch (halfs)
   static constexpr int VPH = 36;                   // V^T image row pitch (halfs)
   static constexpr int KIMG = 32 * KPH;            // halfs per K image
   static constexpr int VIMG = HS * VPH;            // halfs per V^T image
-  static constexpr int STAGE = 3 * KIMG + 2 * VIMG;  // halfs per stage
+  static constexpr int STAGE = SS * KIMG + 2 * VIMG;  // halfs per stage
 };
 
-template <int HS, int NW>
+template <int HS, int NW, int SS>
 __global__ __launch_bounds__(64 * NW) void gpt_attn_x3_kernel(const float* __restrict__ qkv, float* __restrict__ y, int T,
                                                               int C, int heads, float scale) {
-  using LY = AttnLds<HS>;
+  static_assert(SS == 2 || SS == 3, "score operand splits");
+  using LY = AttnLds<HS, SS>;
   constexpr int NB = HS >= 64 ? 1 : 2;  // LDS stages (one for the large heads: 2-3 workgroups per CU)
   constexpr int NKS = HS / 16;           // k16 steps of the score product
   constexpr int NDT = (HS + 31) / 32;    // 32-wide dimension tiles of O
@@ -306,12 +314,21 @@ __global__ __launch_bounds__(64 * NW) void gpt_attn_x3_kernel(const float* __res
   const float* Vg = base + 2 * C + h * HS;
   const int q0 = (grp * NW + wave) * 32;
 
-  Split3 qf[NKS];  // Q^T B fragments: k = head dimension, n = query q0 + li
+  // Q^T B fragments: k = head dimension, n = query q0 + li (SS = 2: only .h / .m are used)
+  Split3 qf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
     float q8[8];
     ld8(Qg + (int64_t)(q0 + li) * ld + 16 * ks + 8 * hh, q8);
-    qf[ks] = split3(q8);
+    if constexpr (SS == 3) {
+      qf[ks] = split3(q8);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        qf[ks].h[e] = (_Float16)q8[e];
+        qf[ks].m[e] = (_Float16)(q8[e] - (float)qf[ks].h[e]);
+      }
+    }
   }
   // staging: K float4 e -> (row e / (HS/4), quad e % (HS/4)); V group e -> (dim e % HS, keys 4 (e / HS) ..)
   float4 kr[NPK], vr[NPV];
@@ -342,16 +359,23 @@ __global__ __launch_bounds__(64 * NW) void gpt_attn_x3_kernel(const float* __res
       if (e < NKE) {
         const int row = e / (HS / 4), c4 = e - row * (HS / 4);
         at_h2 hv[2], mv[2], lv[2];
-        split3x2(kr[i].x, kr[i].y, hv[0], mv[0], lv[0]);
-        split3x2(kr[i].z, kr[i].w, hv[1], mv[1], lv[1]);
+        if constexpr (SS == 3) {
+          split3x2(kr[i].x, kr[i].y, hv[0], mv[0], lv[0]);
+          split3x2(kr[i].z, kr[i].w, hv[1], mv[1], lv[1]);
+        } else {
+          split2x2(kr[i].x, kr[i].y, hv[0], mv[0]);
+          split2x2(kr[i].z, kr[i].w, hv[1], mv[1]);
+        }
         const int o = row * LY::KPH + c4 * 4;
         uint2 u;
         __builtin_memcpy(&u, hv, 8);
         *reinterpret_cast<uint2*>(S0 + o) = u;
         __builtin_memcpy(&u, mv, 8);
         *reinterpret_cast<uint2*>(S0 + LY::KIMG + o) = u;
-        __builtin_memcpy(&u, lv, 8);
-        *reinterpret_cast<uint2*>(S0 + 2 * LY::KIMG + o) = u;
+        if constexpr (SS == 3) {
+          __builtin_memcpy(&u, lv, 8);
+          *reinterpret_cast<uint2*>(S0 + 2 * LY::KIMG + o) = u;
+        }
       }
     }
 #pragma unroll
@@ -362,7 +386,7 @@ __global__ __launch_bounds__(64 * NW) void gpt_attn_x3_kernel(const float* __res
         at_h2 hv[2], lv[2];
         split2x2(vr[i].x, vr[i].y, hv[0], lv[0]);
         split2x2(vr[i].z, vr[i].w, hv[1], lv[1]);
-        const int o = 3 * LY::KIMG + d * LY::VPH + 4 * k4;
+        const int o = SS * LY::KIMG + d * LY::VPH + 4 * k4;
         uint2 u;
         __builtin_memcpy(&u, hv, 8);
         *reinterpret_cast<uint2*>(S0 + o) = u;
@@ -385,8 +409,8 @@ __global__ __launch_bounds__(64 * NW) void gpt_attn_x3_kernel(const float* __res
   for (int t = 0; t < nt; ++t) {
     if (t + 1 < nt) fetch(t + 1);
     const _Float16* K0 = LH + (NB == 2 ? (t & 1) : 0) * LY::STAGE;
-    const _Float16* V0 = K0 + 3 * LY::KIMG;
-    // S^T = K Q^T, six products on pre-split images
+    const _Float16* V0 = K0 + SS * LY::KIMG;
+    // S^T = K Q^T on pre-split images: six products (SS = 3) or f16x3's three (SS = 2)
     mk_f16 s;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
@@ -396,8 +420,14 @@ __global__ __launch_bounds__(64 * NW) void gpt_attn_x3_kernel(const float* __res
       Split3 kf;
       kf.h = *reinterpret_cast<const mk_h8*>(K0 + o);
       kf.m = *reinterpret_cast<const mk_h8*>(K0 + LY::KIMG + o);
-      kf.l = *reinterpret_cast<const mk_h8*>(K0 + 2 * LY::KIMG + o);
-      mfma6s(s, kf, qf[ks]);
+      if constexpr (SS == 3) {
+        kf.l = *reinterpret_cast<const mk_h8*>(K0 + 2 * LY::KIMG + o);
+        mfma6s(s, kf, qf[ks]);
+      } else {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf.m, qf[ks].h, s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf.h, qf[ks].m, s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf.h, qf[ks].h, s, 0, 0, 0);
+      }
     }
     float mt = -INFINITY;
 #pragma unroll
@@ -502,21 +532,30 @@ void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, floa
     const int nq = T / 32;
     // the largest instantiated wave count (10, 5, 4, 3, 2, 1) <= the cap that divides T / 32
     int nw = hs >= 128 ? DDMI_ATTN_NW128 : DDMI_ATTN_NW;
+    if (const char* ne = getenv(hs >= 128 ? "DDMI_ATTN_NW128" : "DDMI_ATTN_NW")) nw = std::max(1, std::min(10, atoi(ne)));
     while (nw > 1 && (nq % nw || (nw > 5 && nw != 10))) --nw;
     const float scale = (float)(1.0 / std::sqrt((double)hs));
     const dim3 grid((unsigned)((int64_t)B * heads * (nq / nw))), block((unsigned)(64 * nw));
-    const size_t lds = (size_t)(hs >= 64 ? 1 : 2) * (3 * 32 * (hs + 8) + 2 * hs * 36) * 2 + (size_t)nw * 32 * sizeof(float);
+    // score operand splits: DDMI_ATTN_SS (read per dispatch; A/B and precision studies) else DDMI_ATTN_SS_DEFAULT
+    const char* se = getenv("DDMI_ATTN_SS");
+    const int ss = se ? atoi(se) : (prec == 2 ? 3 : DDMI_ATTN_SS_DEFAULT);
+    if (ss != 2 && ss != 3) throw std::runtime_error("gpt_attention(f16x3): DDMI_ATTN_SS must be 2 or 3");
+    const size_t lds = (size_t)(hs >= 64 ? 1 : 2) * (ss * 32 * (hs + 8) + 2 * hs * 36) * 2 + (size_t)nw * 32 * sizeof(float);
     auto go = [&](auto HSC) {
       constexpr int HS = decltype(HSC)::value;
-      switch (nw) {
-        case 10: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 10>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
-        case 5: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 5>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
-        case 4: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 4>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
-        case 3: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 3>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
-        case 2: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 2>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
-        case 1: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 1>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
-        default: throw std::runtime_error("gpt_attention(f16x3): no kernel for " + std::to_string(nw) + " waves");
-      }
+      auto go2 = [&](auto SSC) {
+        constexpr int SS = decltype(SSC)::value;
+        switch (nw) {
+          case 10: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 10, SS>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+          case 5: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 5, SS>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+          case 4: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 4, SS>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+          case 3: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 3, SS>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+          case 2: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 2, SS>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+          case 1: hipLaunchKernelGGL((gpt_attn_x3_kernel<HS, 1, SS>), grid, block, lds, st, qkv, y, T, C, heads, scale); break;
+          default: throw std::runtime_error("gpt_attention(f16x3): no kernel for " + std::to_string(nw) + " waves");
+        }
+      };
+      if (ss == 3) go2(std::integral_constant<int, 3>()); else go2(std::integral_constant<int, 2>());
     };
     switch (hs) {
       case 16: go(std::integral_constant<int, 16>()); break;

@@ -617,16 +617,23 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // (wave tile 64 x 64) with one halo buffer, two per CU - 12 % faster on the 64-channel layers,
   // 11 % slower at Cin = 256 (tools/micro/conv_bench). bf16 keeps the 8-wave form (its 64-channel halo
   // chunk would double the 4-wave form's staging registers)
-  const bool sh4 = a.prec == 0 && a.Cin <= 64;
+  bool sh4 = a.prec == 0 && a.Cin <= 64;
+  bool b128 = bn128;
+  // micro-benchmark override, read per dispatch: DDMI_X6_CFG = 1 forces the 4-wave BN = 64 form, 2 the 8-wave BN = 64 form
+  if (const char* ce = getenv("DDMI_X6_CFG")) {
+    const int cf = atoi(ce);
+    if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
+    if (cf == 2) { sh4 = false; b128 = false; }
+  }
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   if (wide) {
-    if (bn128) {
+    if (b128) {
       X6(8, 32, 128, 4, 2, 3, 4, 0);
     } else {
       if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else X6(8, 32, 64, 4, 2, 2, 3, 0);
     }
   } else {
-    if (bn128) {
+    if (b128) {
       X6(16, 16, 128, 4, 2, 3, 4, 0);
     } else {
       if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else X6(16, 16, 64, 4, 2, 2, 3, 0);

@@ -1102,8 +1102,10 @@ class Model {
       ln(w.ln1, X, C, Hb, C, M);
       gemm(w.qkv, Hb, C, M, QKV, 3 * C);
       // softmax(Q K^T / sqrt(hs)) V per (scene, head), one fused launch (attention.hip): fp32 MFMA in the
-      // fp32 mode, f16x3 MFMA (three-way split scores) in the f16x3 / bf16 modes
-      const int aprec = (gemm_mode == DD_GEMM_FP32 || !gpt_attn_x3 || C / 4 > 128 || T % 32 || T > 1024) ? 0 : 1;
+      // fp32 mode, f16x3 MFMA in the f16x3 mode (two-way split scores) and the bf16 mode (three-way)
+      const int aprec = (gemm_mode == DD_GEMM_FP32 || !gpt_attn_x3 || C / 4 > 128 || T % 32 || T > 1024)
+                            ? 0
+                            : (gemm_mode == DD_GEMM_BF16 ? 2 : 1);
       launch("attn", 4.0 * B * T * T * (double)C, [&] { launch_gpt_attention(QKV, B, T, C, 4, Y, aprec, st); });
       gemm(w.proj, Y, C, M, X, C, false, X, C);  // x = x + proj(y)
       ln(w.ln2, X, C, Hb, C, M);

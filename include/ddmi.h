@@ -207,8 +207,9 @@ int dd_op_mha_small(const float* q, const float* k, const float* v, float* out, 
 /* Fused GPT self-attention core (replaces transfuser_backbone.py:386-410, SelfAttention.forward between
  * the qkv projections and `proj`): qkv (B,T,3C) packed q | k | v, y (B,T,C) =
  * softmax(q_h k_h^T / sqrt(C/heads)) v_h per (scene, head). prec 0: fp32 MFMA, T % 64 == 0 and
- * (T/4) % 8 == 0 (T <= 512), C/heads in {16, 32, 64, 128, 256, 512}; prec 1: f16x3 MFMA (the f16x3 / bf16
- * modes), T % 32 == 0, T <= 1024, C/heads in {16, 32, 64, 128}. */
+ * (T/4) % 8 == 0 (T <= 512), C/heads in {16, 32, 64, 128, 256, 512}; prec 1: f16x3 MFMA (the f16x3 mode:
+ * scores on two-way fp16 splits, three products), prec 2: the same with three-way score splits and six products
+ * (the bf16 mode's choice); both T % 32 == 0, T <= 1024, C/heads in {16, 32, 64, 128}. */
 int dd_op_gpt_attention(const float* qkv, float* y, int B, int T, int C, int heads, int prec, void* stream);
 
 #ifdef __cplusplus

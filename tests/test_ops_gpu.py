@@ -422,9 +422,11 @@ def test_gpt_attention(gpu, B, T, C):
                                        (1, 320, 512, 4.0), (2, 64, 128, 1.0), (1, 96, 64, 3.0),
                                        # T / 32 = 8, 16, 24: wave counts 4 / 4 / 4 (not the 10 of T = 320)
                                        (1, 256, 256, 1.0), (1, 512, 128, 1.0), (1, 768, 64, 1.0), (1, 224, 512, 1.0)])
-def test_gpt_attention_f16x3(gpu, B, T, C, amp):
+@pytest.mark.parametrize("prec", [1, 2])
+def test_gpt_attention_f16x3(gpu, B, T, C, amp, prec):
     """The f16x3 GPT attention (flash-style over 32-key tiles, P taken from the S^T accumulators) vs PyTorch
-    fp64; amp scales q / k to sharpen the softmax (scores up to ~|40| at amp 4)."""
+    fp64; amp scales q / k to sharpen the softmax (scores up to ~|40| at amp 4). prec 1: scores on two-way
+    splits (three products), prec 2: three-way splits (six products) - the same fp32-class bar."""
     nh, hs = 4, C // 4
     qkv = rnd(B, T, 3 * C, seed=33)
     qkv[..., : 2 * C] *= amp
@@ -433,7 +435,7 @@ def test_gpt_attention_f16x3(gpu, B, T, C, amp):
     ref = (att @ v).transpose(1, 2).reshape(B, T, C)
     out = torch.empty(B, T, C, device=DEV)
     qd = g(qkv)
-    ok(gpu.dd_op_gpt_attention(qd.data_ptr(), out.data_ptr(), B, T, C, nh, 1, None), gpu)
+    ok(gpu.dd_op_gpt_attention(qd.data_ptr(), out.data_ptr(), B, T, C, nh, prec, None), gpu)
     close(out, ref, 2e-5)
 
 

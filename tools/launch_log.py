@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--arch", default="resnet34")
-    ap.add_argument("--gemm", default="fp32")
+    ap.add_argument("--gemm", default="f16x3")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "launches.md"))
     a = ap.parse_args()
     log = tempfile.NamedTemporaryFile(prefix="ddmi_launch_", suffix=".tsv", delete=False).name
@@ -55,7 +55,7 @@ def main():
     total = 0.0
     with open(log) as f:
         for line in f:
-            name, detail, flops, ms = line.rstrip("\n").split("\t")
+            name, detail, flops, ms = line.rstrip("\n").split("\t")[:4]
             ms = float(ms) / a.reps
             total += ms
             if not detail:

@@ -27,4 +27,11 @@ for C in (64, 128, 256, 512):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
     fl = 4.0 * B * T * T * C
-    print(f"C={C:4d} hs={C // 4:3d}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
+    # float64 reference on 4 scenes: max |err| / max |y|
+    hs = C // 4
+    x = qkv[:4].double().view(4, T, 3, 4, hs)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = torch.softmax(q @ k.transpose(-1, -2) / hs ** 0.5, -1) @ v
+    ref = ref.transpose(1, 2).reshape(4, T, C)
+    err = ((y[:4].double() - ref).abs().max() / ref.abs().max()).item()
+    print(f"C={C:4d} hs={hs:3d}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s  rel err {err:.2e}", flush=True)
