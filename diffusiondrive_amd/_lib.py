@@ -55,6 +55,7 @@ _SIGS = {
                                        ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]),
     "dd_kernel_bytes": (ctypes.c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     "dd_set_seed": (ctypes.c_int, [c_void_p, ctypes.c_ulonglong]),
+    "dd_set_seed_at": (ctypes.c_int, [c_void_p, ctypes.c_ulonglong, ctypes.c_ulonglong]),
     "dd_set_graph": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_set_gemm_mode": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_set_schedule": (ctypes.c_int, [c_void_p, ctypes.c_int]),

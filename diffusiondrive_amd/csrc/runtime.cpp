@@ -1909,12 +1909,14 @@ int dd_kernel_bytes(dd_handle* h, const char* kernel, double* bytes) {
   });
 }
 
-int dd_set_seed(dd_handle* h, unsigned long long seed) {
+int dd_set_seed(dd_handle* h, unsigned long long seed) { return dd_set_seed_at(h, seed, 0); }
+
+int dd_set_seed_at(dd_handle* h, unsigned long long seed, unsigned long long first_scene) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
     std::lock_guard<std::mutex> lk(h->mu);
     h->m->rng_seed = seed;
-    h->m->rng_next = 0;
+    h->m->rng_next = first_scene;
   });
 }
 

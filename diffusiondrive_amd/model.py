@@ -152,9 +152,12 @@ class DiffusionDriveModel:
             raise _lib.DDMIError("numerics flag raised by the fp32 forward as well")
         return out
 
-    def set_seed(self, seed: int):
-        """Seed of the device noise draw (``noise="device"``); restarts its stream (dd_set_seed)."""
-        _lib.check(self.lib.dd_set_seed(self.handle, int(seed) & (2 ** 64 - 1)), self.lib)
+    def set_seed(self, seed: int, first_scene: int = 0):
+        """Seed of the device noise draw (``noise="device"``); restarts its stream at global scene index
+        ``first_scene`` (dd_set_seed_at: a scene shard starting at that index draws the unsharded run's noise)."""
+        if first_scene < 0:
+            raise ValueError("first_scene must be >= 0")
+        _lib.check(self.lib.dd_set_seed_at(self.handle, int(seed) & (2 ** 64 - 1), int(first_scene)), self.lib)
 
     def _forward(self, features, noise, steps, heads, modes, stream) -> Dict[str, torch.Tensor]:
         # stage inputs and allocate outputs on the stream the forward is ordered after, so the caching

@@ -88,6 +88,9 @@ int dd_destroy(dd_handle* h);
 /* Seed of the device noise draw (noise == NULL in dd_forward) and restart of its stream at scene 0. Default
  * seed 0. No reference counterpart (the reference draws on the CPU, transfuser_model_v2.py:593). */
 int dd_set_seed(dd_handle* h, unsigned long long seed);
+/* The same, with the stream positioned at global scene index first_scene: rank r of a scene-sharded job that
+ * passes first_scene = r * (scenes per rank) draws exactly the noise of those scenes in an unsharded run. */
+int dd_set_seed_at(dd_handle* h, unsigned long long seed, unsigned long long first_scene);
 
 /* Last error message of the calling thread ("" if none). */
 const char* dd_last_error(void);

@@ -70,6 +70,23 @@ def test_null_noise_stream_is_chunk_invariant(seeded_sd, monkeypatch):
     assert waypoint_l2(outs[0], outs[1]) <= 1e-5
 
 
+def test_null_noise_shard_equals_unsharded_slice(gpu_model):
+    """dd_set_seed_at: a scene shard whose device-noise stream starts at its global scene index draws exactly the
+    unsharded run's noise for those scenes (the noise tap is compared bit for bit), so the shard's trajectories
+    equal the unsharded run's slice (bit-exact where the kernel routes of B = 6 and B = 3 coincide; 1e-5 bar)."""
+    f, _ = _dev_inputs(6, 23)
+    gpu_model.set_seed(41)
+    full = gpu_model.forward(f, noise="device")["trajectory"].clone()
+    nz_full = gpu_model.tap("in_noise", (6, 20, 8, 2)).clone()
+    gpu_model.set_seed(41, first_scene=3)
+    half = gpu_model.forward({k: v[3:] for k, v in f.items()}, noise="device")["trajectory"].clone()
+    nz_half = gpu_model.tap("in_noise", (3, 20, 8, 2)).clone()
+    assert torch.equal(nz_half, nz_full[3:])
+    assert waypoint_l2(half.cpu().numpy(), full[3:].cpu().numpy()) <= 1e-5
+    with pytest.raises(ValueError):
+        gpu_model.set_seed(41, first_scene=-1)
+
+
 def test_flagged_forward_reruns_in_fp32(gpu_model):
     """An input far outside the fp16 range raises DD_NUM_F16_OVERFLOW in f16x3; forward(safe=True) and the batched
     runner's _finish re-run it on the fp32 path (a warning, the fp32 result, the flag cleared)."""
