@@ -257,6 +257,32 @@ const char* last_conv_config();
 void set_last_conv_config(const char* cfg);
 
 // ----------------------------------------------------------------------------------------
+// The gathered value_proj (value_proj.hip): value rows = ReLU(conv3x3(map) + bias) at the scenes' distinct tap
+// pixels, rows[b * cap + l] (l < counts[b]) = pixel b * 4096 + y * 64 + x of the (B, 64, 64, 256) NHWC map; row
+// b * cap + l of `out` receives it. wh / wl: the f16x3 weight images [256][ldh] (K order kh, kw, ci) with
+// per-column inverse scales wsinv; part: [3][B * cap][256] fp32 scratch; tile_cnt: vproj_tiles(B, cap) zeroed
+// words (left zeroed by every launch).
+struct VprojArgs {
+  const float* map = nullptr;
+  const uint16_t* wh = nullptr;
+  const uint16_t* wl = nullptr;
+  const float* wsinv = nullptr;
+  int ldh = 0;
+  const float* bias = nullptr;
+  const int* rows = nullptr;
+  const int* counts = nullptr;
+  int B = 0, cap = 0;
+  float* part = nullptr;
+  unsigned* tile_cnt = nullptr;
+  float* out = nullptr;
+  unsigned* flags = nullptr;
+  int max_splits = 3;  // 1..3 (DDMI_VPROJ_SPLITS: tests / A/B)
+};
+bool vproj_supported(int C, int Cout, int H, int W);
+size_t vproj_tiles(int B, int cap);
+void launch_vproj(const VprojArgs& a, hipStream_t st);
+
+// ----------------------------------------------------------------------------------------
 // Bandwidth / small kernels (elementwise.hip)
 // NCHW fp32 (B, C, H, W) -> NHWC padded to Cp channels (zero fill).
 void launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int H, int W, int Cp, hipStream_t st);

@@ -454,6 +454,8 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
     if (t == 4) { launch_x5_cfg<2, 2, 2, 2, 4>(a, M, K, st); return true; }   // 128 x 128, 4 waves
     if (t == 5) { launch_x5_cfg<2, 4, 3, 2, 2>(a, M, K, st); return true; }   // 192 x 256, 8 waves
     if (t == 6) { launch_x5_cfg<2, 2, 3, 2, 3>(a, M, K, st); return true; }   // 192 x 128, 4 waves
+    if (t == 7) { launch_x5_cfg<2, 2, 2, 2, 2>(a, M, K, st); return true; }   // 128 x 128, 4 waves, 2 stages (2 per CU)
+    if (t == 99) return false;                                                // conv_x3 / fallback
   }
   const int64_t m256 = (M + 255) / 256;
   const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;

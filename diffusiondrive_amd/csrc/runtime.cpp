@@ -149,6 +149,8 @@ class Model {
   bool value_gather = true;
   bool value_dedup = true;
   bool value_compact = true;         // DDMI_VALUE_COMPACT=0: gathered value rows in per-scene tile runs
+  bool value_splitk = true;          // DDMI_VALUE_SPLITK=0: the gathered value_proj on conv_x3 (one launch, K whole)
+  int vproj_splits = 3;              // DDMI_VPROJ_SPLITS: most K splits of value_proj.hip (1..3)
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
@@ -224,6 +226,8 @@ class Model {
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_COMPACT")) value_compact = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VALUE_SPLITK")) value_splitk = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VPROJ_SPLITS")) vproj_splits = std::max(1, std::min(3, atoi(e)));
     if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
     DD_HIP_CHECK(hipMemset(in_tab, 0, 4 * sizeof(float*)));
@@ -581,6 +585,28 @@ class Model {
       a.rowcap = MR / B;
     }
     const double fl = 2.0 * MR * (double)d * 9 * dl[l].vproj.cin_real;
+    const Conv& vc = dl[l].vproj;
+    if (value_splitk && value_compact && counts && vproj_supported(vc.cin, vc.cout, HB, WB) && a.wh && a.prec == 0) {
+      // value_proj.hip: compacted rows in 256 x 256 tiles, K split up to three ways, deterministic combine
+      VprojArgs v;
+      v.map = cross;
+      v.wh = a.wh;
+      v.wl = a.wl;
+      v.wsinv = a.wsinv;
+      v.ldh = (int)a.ldh;
+      v.bias = a.bias;
+      v.rows = rows;
+      v.counts = counts;
+      v.B = B;
+      v.cap = MR / B;
+      v.part = buf("vproj_part", (size_t)3 * MR * d);
+      v.tile_cnt = reinterpret_cast<unsigned*>(buf_zeroed("vproj_cnt", vproj_tiles(B, MR / B)));
+      v.out = vrows;
+      v.flags = num_flags;
+      v.max_splits = vproj_splits;
+      launch("value_proj", fl, [&] { launch_vproj(v, st); });
+      return;
+    }
     struct ClassScope {
       const char*& c;
       ClassScope(const char*& cc, const char* v) : c(cc) { c = v; }
@@ -700,6 +726,16 @@ class Model {
 
   // ------------------------------------------------------------------ runtime helpers
   const float* W(size_t off) const { return ar.ptr(off); }
+
+  // a workspace buffer whose words start zeroed when it is (re)allocated (allocation only happens in eager,
+  // uncaptured forwards; kernels that use such words leave them zeroed). The memset is ordered on the handle's
+  // stream: that stream is non-blocking, so a plain hipMemset (legacy stream) could land after the first kernels.
+  float* buf_zeroed(const std::string& name, size_t n) {
+    const uint64_t g = generation;
+    float* p = buf(name, n);
+    if (generation != g) DD_HIP_CHECK(hipMemsetAsync(p, 0, std::max<size_t>(n, 4) * sizeof(float), st));
+    return p;
+  }
 
   float* buf(const std::string& name, size_t n) {
     auto it = bufs.find(name);

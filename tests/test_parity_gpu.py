@@ -424,10 +424,13 @@ def test_fused_token_pooling_matches_avgpool(gpu_model, seeded_sd, monkeypatch):
     assert waypoint_l2(out, ref["trajectory"].numpy()) <= 1e-6
 
 
-def test_compacted_value_rows_equal_per_scene_tiles(gpu_model, seeded_sd, monkeypatch):
-    """The gathered value_proj with the scenes' rows compacted into full 128-row tiles (default) against one tile
-    run per scene (DDMI_VALUE_COMPACT=0): every output row is the same dot products in the same K order wherever
-    its tile sits, so every live row and the trajectory are bit-identical."""
+def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
+    """The gathered value_proj on the same inputs: the default kernel (value_proj.hip: compacted rows in 256 x 256
+    tiles, K split up to three ways, the partials summed in split order by the last split), the same kernel held to
+    two and to one split (DDMI_VPROJ_SPLITS), conv_x3 over the compacted rows (DDMI_VALUE_SPLITK=0) and conv_x3
+    with one tile run per scene (+ DDMI_VALUE_COMPACT=0). The two conv_x3 forms evaluate every row with the same
+    dot products in the same K order wherever its tile sits: bit-identical. value_proj.hip differs from them by
+    summation order only: every live row within 1e-5 relative, trajectories within 1e-5."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
     B = 6
@@ -436,28 +439,60 @@ def test_compacted_value_rows_equal_per_scene_tiles(gpu_model, seeded_sd, monkey
     nz = torch.from_numpy(inp["noise"])
     names = [f"s{s}l{l}" for s in range(2) for l in range(2)]
 
-    def run(m):
+    def run(m, profile=False):
+        if profile:
+            m.set_profiling(True)
+            m.reset_stats()
         out = m.forward(feats, noise=nz)["trajectory"].numpy()
+        if profile:
+            assert m.kernel_stats("value_proj")["launches"] == 4
+            m.set_profiling(False)
         taps = {k: (m.tap(f"value_taps_{k}").view(torch.int32).cpu().numpy()[: B * 640],
                     m.tap(f"value_rows_{k}").cpu().numpy()[: B * 640 * 256].reshape(-1, 256)) for k in names}
         assert m.numerics_flags() == 0
         return out, taps
 
+    def fresh(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+        try:
+            return run(m)
+        finally:
+            m.close()
+            for k in env:
+                monkeypatch.delenv(k)
+
     gpu_model.set_gemm_mode("f16x3")
     try:
-        out, got = run(gpu_model)
+        runs = {"splitk3": run(gpu_model, profile=True)}
     finally:
+        gpu_model.set_profiling(False)
         gpu_model.set_gemm_mode("fp32")
-    monkeypatch.setenv("DDMI_VALUE_COMPACT", "0")
-    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
-    ref_out, ref = run(m)
-    m.close()
+    runs["splitk2"] = fresh(DDMI_VPROJ_SPLITS="2")
+    runs["splitk1"] = fresh(DDMI_VPROJ_SPLITS="1")
+    runs["x3"] = fresh(DDMI_VALUE_SPLITK="0")
+    runs["x3_per_scene"] = fresh(DDMI_VALUE_SPLITK="0", DDMI_VALUE_COMPACT="0")
+    ref_out, ref = runs["x3"]
+    lines = ["== gathered value_proj: value_proj.hip (3 / 2 / 1 splits) vs conv_x3 (compacted / per scene)"]
     for k in names:
-        rows, vals = got[k]
+        rows = ref[k][0]
         live = rows >= 0
-        assert np.array_equal(rows, ref[k][0]), k
-        assert np.array_equal(vals[live], ref[k][1][live]), k
-    assert np.array_equal(out, ref_out)
+        assert np.array_equal(rows, runs["x3_per_scene"][1][k][0]), k
+        assert np.array_equal(ref[k][1][live], runs["x3_per_scene"][1][k][1][live]), k
+        for v in ("splitk3", "splitk2", "splitk1"):
+            got = runs[v][1][k]
+            assert np.array_equal(rows, got[0]), (v, k)
+            r = ref[k][1][live]
+            err = float(np.abs(got[1][live] - r).max() / max(1.0, np.abs(r).max()))
+            lines.append(f"  {k} {v}: {int(live.sum())} live rows, max rel err vs conv_x3 {err:.3e}")
+            assert err <= 1e-5, (v, k, err)
+    assert np.array_equal(ref_out, runs["x3_per_scene"][0])
+    for v in ("splitk3", "splitk2", "splitk1"):
+        l2 = waypoint_l2(runs[v][0], ref_out)
+        lines.append(f"  trajectory waypoint L2 {v} vs conv_x3 {l2:.3e}")
+        assert l2 <= 1e-5, (v, l2)
+    _report(lines)
 
 
 @pytest.mark.parametrize("mode", ["f16x3", "bf16"])

@@ -51,6 +51,9 @@ static const Shape kShapes[] = {
     {"gpt.proj3", 64 * 320, 1, 1, 256, 256, 1, 1, 1},
     {"img.l4.s2", 64, 16, 64, 256, 512, 3, 2, 0},
     {"img.l4.ds", 64, 16, 64, 256, 512, 1, 2, 0},
+    {"img.l2.ds", 64, 64, 256, 64, 128, 1, 2, 0},
+    {"img.l3.s2", 64, 32, 128, 128, 256, 3, 2, 0},
+    {"img.l3.ds", 64, 32, 128, 128, 256, 1, 2, 0},
     {"lid.l4.3x3", 64, 8, 8, 512, 512, 3, 1, 1},
     // fixed-cost probes: the img.l2 / img.l3 tiles with the K walk halved / doubled
     {"fx.l3.c128", 64, 16, 64, 128, 256, 3, 1, 1},
