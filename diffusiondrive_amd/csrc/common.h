@@ -277,6 +277,7 @@ struct VprojArgs {
   float* out = nullptr;
   unsigned* flags = nullptr;
   int max_splits = 3;  // 1..3 (DDMI_VPROJ_SPLITS: tests / A/B)
+  int max_wgs = 256;   // workgroup budget for (tiles x splits): the CUs not held by a concurrent kernel
 };
 bool vproj_supported(int C, int Cout, int H, int W);
 size_t vproj_tiles(int B, int cap);

@@ -570,8 +570,9 @@ class Model {
   // counts (nullable): the scenes' live-row counts - the launch then runs the scenes' rows compacted (full
   // 128-row tiles; DDMI_VALUE_COMPACT=0 keeps one tile run per scene). Timed under its own class "value_proj";
   // its FLOPs count every row slot (2 x slots x 256 x 2304; bench.py derives the live-row rate from the counts).
+  // busy_cus: CUs a kernel on the other branch holds meanwhile (the tf-decoder megakernel: one per scene)
   void gathered_value(int l, const int* rows, const int* counts, float* vrows, const float* cross, int B, int HB,
-                      int WB, int MR) {
+                      int WB, int MR, int busy_cus = 0) {
     const int d = 256;
     ConvArgs a = conv_args(dl[l].vproj, cross, (int64_t)HB * WB * d, (int64_t)WB * d, d, B, HB, WB, vrows,
                            (int64_t)MR * d, d, 0, true, nullptr, 0, 0, 0);
@@ -604,6 +605,7 @@ class Model {
       v.out = vrows;
       v.flags = num_flags;
       v.max_splits = vproj_splits;
+      v.max_wgs = std::max(64, num_cus() - busy_cus);
       launch("value_proj", fl, [&] { launch_vproj(v, st); });
       return;
     }
@@ -666,7 +668,7 @@ class Model {
       for (int l = 0; l < 2; ++l) {
         const std::string sf = sfx(si, l);
         float* vrows = buf("value_rows" + sf, (size_t)MR * d);
-        gathered_value(l, rows_of(si, l), counts_of(si, l), vrows, cross, B, HB, WB, MR);
+        gathered_value(l, rows_of(si, l), counts_of(si, l), vrows, cross, B, HB, WB, MR, tf_pending ? B : 0);
         if (tf_pending) {
           join();  // tf decoder: agent K / V and ego rows of both layers
           tf_pending = false;
@@ -726,6 +728,16 @@ class Model {
 
   // ------------------------------------------------------------------ runtime helpers
   const float* W(size_t off) const { return ar.ptr(off); }
+
+  int num_cus() {
+    if (!cu_count) {
+      int dev = 0;
+      DD_HIP_CHECK(hipGetDevice(&dev));
+      DD_HIP_CHECK(hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    return cu_count;
+  }
+  int cu_count = 0;
 
   // a workspace buffer whose words start zeroed when it is (re)allocated (allocation only happens in eager,
   // uncaptured forwards; kernels that use such words leave them zeroed). The memset is ordered on the handle's

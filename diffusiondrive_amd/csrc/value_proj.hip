@@ -10,9 +10,9 @@
 // ~249 workgroups - one wave. (An earlier 128 x 256 form with the same split ran 498 workgroups, 1.95 waves, and
 // was 20 % slower than conv_x3: profiles/round3_f_vproj_splitk_ab.txt.)
 //
-// Splits: S = the largest of 3, 2, 1 with (live tiles) x S <= 256, decided in the kernel from the live-row count
-// (known only on the device); split s of S takes K chunks [72 s / S, 72 (s + 1) / S) of the 72 (9 taps x 8 channel
-// chunks of 32).
+// Splits: S = the largest of 3, 2, 1 with (live tiles) x S <= the CU budget (256, or 192 while the tf-decoder
+// megakernel holds 64 CUs beside the first launch), decided in the kernel from the live-row count (known only on the
+// device); split s of S takes K chunks [72 s / S, 72 (s + 1) / S) of the 72 (9 taps x 8 channel chunks of 32).
 //
 // Per workgroup: 8 waves (4 x 2, wave tile 64 x 128), A = the tile's gathered rows by LDS-DMA (per-lane 16-B
 // buffer loads at each row's own pixel offset; out-of-map taps read zero through the out-of-range offset), B = the
@@ -92,9 +92,10 @@ __device__ inline void vp_split8(const float4& p, const float4& q, vp_h8& hi, vp
 // cache-policy bits of the raw buffer intrinsics: sc1 (write-through stores, L1-bypassing loads)
 constexpr int kSC1 = 16;
 
-// splits for a launch with `tiles` live 256-row tiles: the most (<= 3) that keep the grid within one wave
-__device__ inline int vp_splits(int tiles, int cap) {
-  const int s = tiles * 3 <= 256 ? 3 : (tiles * 2 <= 256 ? 2 : 1);
+// splits for a launch with `tiles` live 256-row tiles: the most (<= 3) that keep the grid within one wave of the
+// `budget` CUs this launch has (the whole chip, or what a concurrent kernel leaves: one workgroup per CU here)
+__device__ inline int vp_splits(int tiles, int cap, int budget) {
+  const int s = tiles * 3 <= budget ? 3 : (tiles * 2 <= budget ? 2 : 1);
   return s < cap ? s : cap;
 }
 
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   rowcount_prefix(a.counts, a.B, g_pre);
   const int total = g_pre[a.B];
   const int tiles = (total + VP_BM - 1) / VP_BM;
-  const int S = vp_splits(tiles, a.max_splits);
+  const int S = vp_splits(tiles, a.max_splits, a.max_wgs);
   const int bid = blockIdx.x;
   if (bid >= tiles * S) return;  // workgroup-uniform; touches no counter
   const int mt = bid / S, sp = bid - mt * S;
@@ -342,7 +343,8 @@ size_t vproj_tiles(int B, int cap) { return ((size_t)B * cap + VP_BM - 1) / VP_B
 void launch_vproj(const VprojArgs& a, hipStream_t st) {
   if (!a.map || !a.wh || !a.wl || !a.wsinv || !a.bias || !a.rows || !a.counts || !a.part || !a.tile_cnt || !a.out)
     throw std::runtime_error("vproj: missing operand");
-  if (a.B < 1 || a.B > 256 || a.cap < 1 || a.ldh < 9 * kC || a.ldh % 8 || a.max_splits < 1 || a.max_splits > 3)
+  if (a.B < 1 || a.B > 256 || a.cap < 1 || a.ldh < 9 * kC || a.ldh % 8 || a.max_splits < 1 || a.max_splits > 3 ||
+      a.max_wgs < 1)
     throw std::runtime_error("vproj: B in [1, 256], ldh >= 2304 and a multiple of 8, max_splits in [1, 3]");
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!al16(a.map) || !al16(a.wh) || !al16(a.wl) || !al16(a.wsinv) || !al16(a.bias) || !al16(a.part) || !al16(a.out))

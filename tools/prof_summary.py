@@ -25,6 +25,10 @@ def kclass(name):
     n = name.replace("(anonymous namespace)::", "").split("(")[0]
     n = re.sub(r"^void\s+", "", n)
     n = n.replace("ddmi::", "")
+    # the gathered value_proj (value_proj.hip, or conv_x3's GATHER = 1 instance): its own class, as in
+    # tools/pmc_round2.py, so the trace and PMC summaries join per class (tools/roofline_table.py)
+    if re.match(r"conv_x3_kernel<(\s*\d+\s*,){6}\s*1\s*>", n) or n.startswith("vproj_kernel"):
+        return "value_proj"
     n = re.sub(r"<.*>", "", n)
     return n.replace("_kernel", "")
 
