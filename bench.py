@@ -11,9 +11,13 @@ environment, nothing touches the GPU before that) and exits with the worst rank'
 ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` each rank reads the
 launcher's environment; a ``--gpus`` that disagrees with ``$WORLD_SIZE`` is an error.
 
-A step = one forward of B synthetic scenes resident in HBM (+ the all_gather when N > 1).
+A step = one forward of B synthetic scenes resident in HBM (+ the all_gather when N > 1). ``--in-flight L``
+(default 3) keeps L steps in flight per GPU (diffusiondrive_amd/model.py InFlightPlanner); the timed region
+still brackets all K steps completely.
 Rank 0 prints ONE JSON line. Besides the contract fields it reports:
-  * ``median_ms_per_step``: median of the per-step HIP-event durations of the timed loop;
+  * ``median_ms_per_step``: median interval between consecutive step completions (HIP events on the lanes'
+    streams); ``median_batch_latency_ms``: median start -> end of one step's forward on its lane (with
+    ``--in-flight N`` > 1, N batches share the device, so a batch takes longer while the steps complete faster);
   * ``fp32_leg``: the same workload on the fp32-MFMA path (N = 1), the conservative headline;
   * ``h2d_included``: the same forward with its inputs copied from pinned host memory every
     step (PCIe-inclusive; never ``value``);
@@ -87,6 +91,9 @@ def parse():
     p.add_argument("--gemm", default="f16x3", choices=["fp32", "f16x3", "bf16"],
                    help="conv/linear arithmetic: fp32 MFMA, the fp32-class 3-product fp16 split, or bf16")
     p.add_argument("--no-compare", action="store_true", help="skip the fp32 leg and the H2D-inclusive leg")
+    p.add_argument("--in-flight", type=int, default=3,
+                   help="batches in flight per GPU (InFlightPlanner lanes: single-stream handles on streams of their "
+                        "own); 1 = one two-stream forward at a time")
     p.add_argument("--cpu-plumbing", action="store_true",
                    help="tests only: launcher + gloo all_gather + JSON with a stand-in step (no forward)")
     return p.parse_args()
@@ -138,56 +145,77 @@ def main():
 
     from diffusiondrive_amd.config import TransfuserConfig
     from diffusiondrive_amd.dist import ScenePlanner
-    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.model import InFlightPlanner
     from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
 
+    if args.in_flight < 1:
+        print("[bench] --in-flight must be >= 1", file=sys.stderr)
+        sys.exit(2)
     cfg = TransfuserConfig(image_architecture=args.arch)
     sd = seeded_state_dict(cfg, 0)
-    model = DiffusionDriveModel(cfg, sd, device=local)
-    model.set_gemm_mode(args.gemm)
+    # args.in_flight lanes (handles with the same weights); lane 0 also serves the profiled replay
+    pl = InFlightPlanner(cfg, sd, device=local, lanes=args.in_flight)
+    pl.set_gemm_mode(args.gemm)
+    model = pl.lanes[0]
     B = args.batch
     inp = synthetic_inputs(B, 1234 + rank, cfg)
     keys = ("camera_feature", "lidar_feature", "status_feature")
     feats = {k: torch.from_numpy(inp[k]).to(dev) for k in keys}
     noise = torch.from_numpy(inp["noise"]).to(dev)
-    planner = ScenePlanner(lambda f, nz: model.forward(f, noise=nz, steps=args.denoise_steps)["trajectory"])
+    planner = ScenePlanner(lambda f, nz: pl.forward(f, noise=nz, steps=args.denoise_steps)["trajectory"])
+    marks = []  # per step: (start, end) HIP events on the stream the step ran on
+
+    def lane_step(body):
+        # the next lane: its forward and the all_gather of its trajectories on the lane's stream
+        with pl.next_lane() as m:
+            s = torch.cuda.current_stream(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            o = planner.gather(body(m, s))
+            e1.record(s)
+            marks.append((e0, e1))
+            return o
 
     def step():
         # per-rank shard of the global batch (weak scaling) + one RCCL all_gather of trajectories
-        return planner.gather(planner.fn(feats, noise))
+        return lane_step(lambda m, s: m.forward(feats, noise=noise, steps=args.denoise_steps, stream=s)["trajectory"])
 
     def timed(fn, k):
-        """k steps between barrier + synchronize; per-step HIP events on the current stream."""
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)]
+        """k steps between barrier + synchronize. Per step: the interval between consecutive step completions
+        (HIP events on the lanes' streams, one device clock) and the batch latency (its own start -> end)."""
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+        marks.clear()
+        e_start = torch.cuda.Event(enable_timing=True)
+        e_start.record()
         t0 = time.perf_counter()
-        ev[0].record()
         o = None
-        for i in range(k):
+        for _ in range(k):
             o = fn()
-            ev[i + 1].record()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         el = time.perf_counter() - t0
-        per = [ev[i].elapsed_time(ev[i + 1]) for i in range(k)]
-        return o, el, per
+        ends = [e_start] + [e1 for _, e1 in marks]
+        per = [ends[i].elapsed_time(ends[i + 1]) for i in range(len(ends) - 1)]
+        lat = [e0.elapsed_time(e1) for e0, e1 in marks]
+        return o, el, per, lat
 
     for _ in range(args.warmup):
         out = step()
     torch.cuda.synchronize()
-    out, elapsed, per_step = timed(step, args.steps)
+    out, elapsed, per_step, lat_step = timed(step, args.steps)
     med = float(np.median(per_step))
+    lat_med = float(np.median(lat_step))
     if dist is not None:
-        t = torch.tensor([elapsed, med], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, med, lat_med], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, med = float(t[0].item()), float(t[1].item())
+        elapsed, med, lat_med = float(t[0].item()), float(t[1].item()), float(t[2].item())
     ms_per_step = elapsed / args.steps * 1e3
     scenes_per_s = B * world * args.steps / elapsed
     traj_gpu = out[rank * B:(rank + 1) * B].detach().cpu().numpy()
-    num_flags = model.numerics_flags()
+    num_flags = pl.numerics_flags()
     if num_flags:
         print(f"[bench] WARNING: numerics flags {num_flags:#x} raised (f16x3 overflow): result untrustworthy",
               file=sys.stderr)
@@ -214,35 +242,52 @@ def main():
     executed_flops = sum(v["flops"] for v in conv_stats.values()) + other["attn"]["flops"] + other["value_proj"]["flops"]
     executed_gflop_scene = executed_flops / prof_steps / B / 1e9
 
-    fp32_leg = h2d = None
+    fp32_leg = h2d = one_at_a_time = None
     if world == 1 and not args.no_compare:
         # the fp32-MFMA path on the same workload (the conservative headline)
         other_mode = "fp32" if args.gemm != "fp32" else "f16x3"
-        model.set_gemm_mode(other_mode)
-        for _ in range(2):
+        pl.set_gemm_mode(other_mode)
+        for _ in range(2 * args.in_flight):
             step()
         n_cmp = max(5, min(args.steps // 2, 30))
-        o2, dt, per2 = timed(step, n_cmp)
+        o2, dt, per2, _ = timed(step, n_cmp)
         fp32_leg = {"gemm": other_mode, "value": round(B * n_cmp / dt, 3), "ms_per_step": round(dt / n_cmp * 1e3, 3),
                     "median_ms_per_step": round(float(np.median(per2)), 3), "steps": n_cmp,
-                    "traj": o2.detach().cpu().numpy()}
-        model.set_gemm_mode(args.gemm)
-        # PCIe-inclusive: inputs staged from pinned host memory every step
+                    "in_flight": args.in_flight, "traj": o2.detach().cpu().numpy()}
+        pl.set_gemm_mode(args.gemm)
+        if args.in_flight > 1:
+            # one batch at a time on lane 0 as a two-stream handle (the --in-flight 1 configuration)
+            model.set_streams(2)
+            for _ in range(3):
+                model.forward(feats, noise=noise, steps=args.denoise_steps)
+            n1 = max(5, min(args.steps // 2, 60))
+            _, dt1, _, _ = timed(lambda: model.forward(feats, noise=noise, steps=args.denoise_steps)["trajectory"], n1)
+            one_at_a_time = {"value": round(B * n1 / dt1, 3), "ms_per_step": round(dt1 / n1 * 1e3, 3), "steps": n1,
+                             "note": "in_flight 1: one two-stream forward at a time (its ms_per_step is the batch "
+                                     "latency of that mode)"}
+            model.set_streams(1)
+        # PCIe-inclusive: inputs staged from pinned host memory every step (one device buffer set per lane)
         host = {k: torch.from_numpy(inp[k]).pin_memory() for k in keys}
         host_nz = torch.from_numpy(inp["noise"]).pin_memory()
-        dbuf = {k: torch.empty_like(v, device=dev) for k, v in host.items()}
-        dnz = torch.empty_like(host_nz, device=dev)
+        dbufs = [({k: torch.empty_like(v, device=dev) for k, v in host.items()}, torch.empty_like(host_nz, device=dev))
+                 for _ in range(args.in_flight)]
+        h2d_i = [0]
 
         def step_h2d():
-            for k in keys:
-                dbuf[k].copy_(host[k], non_blocking=True)
-            dnz.copy_(host_nz, non_blocking=True)
-            return model.forward(dbuf, noise=dnz, steps=args.denoise_steps)["trajectory"]
+            dbuf, dnz = dbufs[h2d_i[0] % args.in_flight]
+            h2d_i[0] += 1
 
-        for _ in range(2):
+            def body(m, s):
+                for k in keys:
+                    dbuf[k].copy_(host[k], non_blocking=True)
+                dnz.copy_(host_nz, non_blocking=True)
+                return m.forward(dbuf, noise=dnz, steps=args.denoise_steps, stream=s)["trajectory"]
+            return lane_step(body)
+
+        for _ in range(2 * args.in_flight):
             step_h2d()
         n_h = max(5, min(args.steps // 2, 40))
-        _, dt, per3 = timed(step_h2d, n_h)
+        _, dt, per3, _ = timed(step_h2d, n_h)
         h2d = {"value": round(B * n_h / dt, 3), "ms_per_step": round(dt / n_h * 1e3, 3),
                "median_ms_per_step": round(float(np.median(per3)), 3), "steps": n_h,
                "bytes_per_step": int(sum(v.numel() * 4 for v in host.values()) + host_nz.numel() * 4),
@@ -271,6 +316,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "median_ms_per_step": round(med, 3),
+        "median_batch_latency_ms": round(lat_med, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -285,6 +331,11 @@ def main():
             "denoise_steps": args.denoise_steps,
             "parallelism": f"dp{world} (scene sharding, RCCL all_gather of trajectories)",
             "graph": True,
+            "in_flight": args.in_flight,
+            "in_flight_note": "batches in flight per GPU: InFlightPlanner lanes (handles with the same weights, each "
+                              "a single-stream captured forward replayed on a stream of its own); consecutive steps "
+                              "go to consecutive lanes; every step's forward runs whole inside the timed region. "
+                              "1 = one two-stream forward at a time",
             "gemm": args.gemm,
             "heads": False,
             "heads_note": "the timed forward is the waypoint path (trajectory out); the BEV-semantic and agent "
@@ -340,6 +391,8 @@ def main():
     }
     if h2d is not None:
         result["h2d_included"] = h2d
+    if one_at_a_time is not None:
+        result["in_flight_1"] = one_at_a_time
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ref = cpu_baseline(args, cfg, sd, inp)

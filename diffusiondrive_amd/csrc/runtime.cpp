@@ -140,6 +140,7 @@ class Model {
   std::map<std::string, KStat> stats;
   hipStream_t st = nullptr;   // the stream launches go to (the handle's main stream, or a side stream)
   hipStream_t st_main = nullptr, st_side = nullptr;  // the handle's own non-blocking streams (capturable)
+  hipStream_t st_own = nullptr;                       // st_main as created (OnStream swaps st_main for a forward)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   // fork / join events of one forward (reused across forwards: every record precedes its wait)
   std::vector<hipEvent_t> fj_ev;
@@ -221,7 +222,7 @@ class Model {
     // in the B = 64 bench graph, both at the least priority 33 % slower
     DD_HIP_CHECK(hipStreamCreateWithFlags(&st_main, hipStreamNonBlocking));
     DD_HIP_CHECK(hipStreamCreateWithFlags(&st_side, hipStreamNonBlocking));
-    st = st_main;
+    st = st_own = st_main;
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
@@ -1719,12 +1720,32 @@ class Model {
     if (!noise) rng_next += (uint64_t)B;
   }
 
+  // Single-stream forwards (dd_set_streams(h, 1)) called on a non-default stream run on the CALLER's stream
+  // itself: no hand-off through the handle's own stream, so N handles driven from N caller streams (N batches
+  // in flight) occupy N hardware queues, not 2N (the device has 4 per process by default; streams beyond them
+  // share queues and serialise). Restores the handle's stream on exit.
+  struct OnStream {
+    Model& m;
+    bool direct;
+    OnStream(Model& mm, hipStream_t caller) : m(mm), direct(!mm.use_side && caller != nullptr && !mm.profiling) {
+      if (direct) {
+        m.st_main = caller;
+        m.st = caller;
+      } else {
+        // order the handle's stream after the caller's stream, run everything there, then hand back
+        DD_HIP_CHECK(hipEventRecord(m.ev_in, caller));
+        DD_HIP_CHECK(hipStreamWaitEvent(m.st, m.ev_in, 0));
+      }
+    }
+    ~OnStream() {
+      if (direct) m.st = m.st_main = m.st_own;
+    }
+  };
+
   void forward_chunk(const float* camera, const float* lidar, const float* status, const float* noise, int B,
                      int steps, const Outs& o, hipStream_t caller, uint64_t scene0) {
     DD_HIP_CHECK(hipSetDevice(device));
-    // order the handle's stream after the caller's stream, run everything there, then hand back
-    DD_HIP_CHECK(hipEventRecord(ev_in, caller));
-    DD_HIP_CHECK(hipStreamWaitEvent(st, ev_in, 0));
+    OnStream on(*this, caller);
     const bool heads = o.sem || o.ag_states || o.ag_labels;
     const uint64_t gen0 = generation;
     stage_inputs(camera, lidar, status, noise, B, scene0);
@@ -1772,8 +1793,9 @@ class Model {
       copy_out(o.ag_states, "agent_states", (size_t)B * 30 * 5);
       copy_out(o.ag_labels, "agent_labels", (size_t)B * 30);
     }
+    // ev_out marks the end of this forward on whichever stream it ran (dd_numerics_flags / dd_tap wait for it)
     DD_HIP_CHECK(hipEventRecord(ev_out, st));
-    DD_HIP_CHECK(hipStreamWaitEvent(caller, ev_out, 0));
+    if (!on.direct) DD_HIP_CHECK(hipStreamWaitEvent(caller, ev_out, 0));
     if (profiling) collect();
   }
 };
@@ -1881,6 +1903,19 @@ int dd_set_profiling(dd_handle* h, int enable) {
   });
 }
 
+int dd_set_streams(dd_handle* h, int n) {
+  return guarded([&] {
+    if (!h) throw std::invalid_argument("null handle");
+    if (n != 1 && n != 2) throw std::invalid_argument("dd_set_streams: n must be 1 or 2");
+    Model& m = *h->m;
+    if (m.use_side == (n == 2)) return;
+    DD_HIP_CHECK(hipStreamSynchronize(m.st));
+    for (auto& g : m.graphs) DD_HIP_CHECK(hipGraphExecDestroy(g.second));  // captured with the other topology
+    m.graphs.clear();
+    m.use_side = n == 2;
+  });
+}
+
 int dd_set_graph(dd_handle* h, int enable) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
@@ -1922,8 +1957,12 @@ int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear) {
     Model& m = *h->m;
     DD_HIP_CHECK(hipSetDevice(m.device));
     DD_HIP_CHECK(hipStreamSynchronize(m.st));
+    DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a single-stream forward may have run on the caller's stream
     DD_HIP_CHECK(hipMemcpy(flags, m.num_flags, sizeof(unsigned), hipMemcpyDeviceToHost));
-    if (clear) DD_HIP_CHECK(hipMemset(m.num_flags, 0, sizeof(unsigned)));
+    if (clear) {
+      DD_HIP_CHECK(hipMemset(m.num_flags, 0, sizeof(unsigned)));
+      DD_HIP_CHECK(hipStreamSynchronize(nullptr));  // cleared before any later forward's kernels run
+    }
   });
 }
 
@@ -1987,6 +2026,7 @@ int dd_tap(dd_handle* h, const char* name, float* dst, size_t count, size_t* act
     }
     if (actual) *actual = n;
     if (dst && count) {
+      DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // the last forward, on whichever stream it ran
       DD_HIP_CHECK(hipMemcpyAsync(dst, src, std::min(n, count) * sizeof(float), hipMemcpyDeviceToDevice,
                                   static_cast<hipStream_t>(stream)));
       DD_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));

@@ -7,10 +7,11 @@
 ``heads=True``). The forward runs entirely in ``libddmi.so`` on the GPU; PyTorch only provides
 device memory and the stream. There is no CPU fallback: without the library or a GPU it raises.
 """
+import contextlib
 import ctypes
 import os
 import warnings
-from typing import Dict, Mapping, Optional
+from typing import Dict, List, Mapping, Optional
 
 import numpy as np
 import torch
@@ -266,6 +267,12 @@ class DiffusionDriveModel:
     def set_graph(self, on: bool):
         _lib.check(self.lib.dd_set_graph(self.handle, int(on)), self.lib)
 
+    def set_streams(self, n: int):
+        """2 (default): the captured forward runs its independent branches (LiDAR trunk, tf decoder, heads) on a
+        second stream; 1: one stream, and a forward called on a non-default stream runs on that stream itself
+        (dd_set_streams; the per-lane mode of InFlightPlanner)."""
+        _lib.check(self.lib.dd_set_streams(self.handle, int(n)), self.lib)
+
     def reset_stats(self):
         _lib.check(self.lib.dd_reset_stats(self.handle), self.lib)
 
@@ -276,3 +283,81 @@ class DiffusionDriveModel:
         by = ctypes.c_double()
         _lib.check(self.lib.dd_kernel_bytes(self.handle, kernel.encode(), ctypes.byref(by)), self.lib)
         return {"ms": ms.value, "launches": n.value, "flops": fl.value, "bytes": by.value}
+
+
+class InFlightPlanner:
+    """N batches in flight on one device: N handles with the same weights, each a single-stream captured forward
+    driven from a stream of its own (dd_set_streams(1): the graph replays on that stream, one hardware queue per
+    lane). Consecutive forwards go to consecutive lanes, so one batch's low-occupancy phases (the one-workgroup-
+    per-scene decoder megakernels, the GPT stages, kernel ramps and tails) overlap the next batches' trunks.
+    Throughput rises, the latency of each batch grows; the results are those of a single-stream forward, lane for
+    lane bit-identical (tests/test_inflight_gpu.py). lanes = 1 is the plain two-stream handle on the caller's
+    stream. No reference counterpart (the reference runs one eager forward at a time).
+
+    Outputs are produced on the lane's stream: read them after ``synchronize()`` (or ``wait()``, which makes the
+    current stream wait for every lane); each forward first waits for the work already queued on the current
+    stream (its inputs)."""
+
+    def __init__(self, config: Optional[TransfuserConfig] = None, state_dict: Optional[Mapping] = None,
+                 device: Optional[int] = None, gemm: Optional[str] = None, lanes: int = 2):
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        self.lanes: List[DiffusionDriveModel] = [DiffusionDriveModel(config, state_dict, device, gemm)
+                                                 for _ in range(lanes)]
+        self.device = self.lanes[0].device
+        if lanes > 1:
+            for m in self.lanes:
+                m.set_streams(1)
+        self.streams = [torch.cuda.Stream(torch.device(f"cuda:{self.device}")) for _ in range(lanes)] \
+            if lanes > 1 else [None]
+        self._next = 0
+
+    def __len__(self):
+        return len(self.lanes)
+
+    @contextlib.contextmanager
+    def next_lane(self):
+        """The next lane's model with the current stream set to that lane's stream (which first waits for the
+        caller's stream); work issued inside (the forward, a collective on its outputs) is ordered on the lane."""
+        i = self._next
+        self._next = (i + 1) % len(self.lanes)
+        s = self.streams[i]
+        if s is None:
+            yield self.lanes[i]
+            return
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            yield self.lanes[i]
+
+    def forward(self, features: Dict[str, torch.Tensor], noise: Optional[torch.Tensor] = None,
+                steps: Optional[int] = None, heads: bool = False, modes: bool = False) -> Dict[str, torch.Tensor]:
+        with self.next_lane() as m:
+            return m.forward(features, noise=noise, steps=steps, heads=heads, modes=modes,
+                             stream=torch.cuda.current_stream(self.device))
+
+    __call__ = forward
+
+    def wait(self):
+        """Make the current stream wait for every lane's queued work."""
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            if s is not None:
+                cur.wait_stream(s)
+
+    def synchronize(self):
+        for s in self.streams:
+            (s or torch.cuda.current_stream(self.device)).synchronize()
+
+    def set_gemm_mode(self, mode: str):
+        for m in self.lanes:
+            m.set_gemm_mode(mode)
+
+    def numerics_flags(self, clear: bool = True) -> int:
+        f = 0
+        for m in self.lanes:
+            f |= m.numerics_flags(clear)
+        return f
+
+    def close(self):
+        for m in self.lanes:
+            m.close()

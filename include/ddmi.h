@@ -107,6 +107,13 @@ int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long lon
 int dd_kernel_bytes(dd_handle* h, const char* kernel, double* bytes);
 /* Enable / disable hipGraph capture + replay of the forward (default on). */
 int dd_set_graph(dd_handle* h, int enable);
+/* Streams of the captured forward: 2 (default; $DDMI_STREAMS=0 at dd_create gives 1) = the LiDAR trunk, the
+ * tf decoder and the optional heads on a second stream beside the rest; 1 = everything in order on one stream,
+ * and a forward called on a non-default stream runs on that stream itself (no hand-off through the handle's
+ * own stream). The batches-in-flight mode: N single-stream handles driven from N caller streams keep N forwards
+ * in flight on one device, one hardware queue each (diffusiondrive_amd/model.py InFlightPlanner). No reference
+ * counterpart (the reference runs one eager forward at a time). */
+int dd_set_streams(dd_handle* h, int n);
 /* GEMM arithmetic of every conv / linear of the path:
  *   DD_GEMM_FP32   fp32-input MFMA (v_mfma_f32_32x32x2_f32), an exact fp32 fma chain;
  *   DD_GEMM_F16X3  3-product fp16 split on f16 MFMA (conv_x3.hip): each fp32 operand becomes
