@@ -279,6 +279,7 @@ class Model {
   }
 
   ~Model() {
+    if (ev_out) (void)hipEventSynchronize(ev_out);  // the last forward, also when it ran on a caller's stream
     if (st_main) (void)hipStreamSynchronize(st_main);
     if (st_side) (void)hipStreamSynchronize(st_side);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
@@ -1910,6 +1911,7 @@ int dd_set_streams(dd_handle* h, int n) {
     Model& m = *h->m;
     if (m.use_side == (n == 2)) return;
     DD_HIP_CHECK(hipStreamSynchronize(m.st));
+    DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a graph replayed on a caller's stream may still run
     for (auto& g : m.graphs) DD_HIP_CHECK(hipGraphExecDestroy(g.second));  // captured with the other topology
     m.graphs.clear();
     m.use_side = n == 2;

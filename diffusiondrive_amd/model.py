@@ -93,8 +93,26 @@ class DiffusionDriveModel:
         del buf
         self.close()
         self._h = h
+        self._blob = blob  # clone() re-creates a handle from it (batches-in-flight lanes)
         self.set_gemm_mode(self._gemm)
         return self
+
+    def clone(self) -> "DiffusionDriveModel":
+        """Another handle on the same device with the same weights, gemm mode and schedule (its own buffers,
+        streams and captured graphs): a lane of InFlightPlanner / the batched runner."""
+        if getattr(self, "_blob", None) is None:
+            raise RuntimeError("DiffusionDriveModel has no weights loaded (call load_state_dict)")
+        m = DiffusionDriveModel(self.config, device=self.device, gemm=self.gemm_mode())
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(self._blob, len(self._blob))
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.dd_create(ctypes.byref(make_dd_config(self.config)), ctypes.cast(buf, ctypes.c_void_p),
+                                          len(self._blob), self.device, ctypes.byref(h)), self.lib)
+        m._h, m._blob = h, self._blob
+        m.set_gemm_mode(m._gemm)
+        if getattr(self, "_schedule", None):
+            m.set_schedule(self._schedule)
+        return m
 
     def close(self):
         if self._h is not None and self._h.value:
@@ -249,6 +267,7 @@ class DiffusionDriveModel:
         if schedule not in self.SCHEDULES:
             raise ValueError(f"schedule must be one of {sorted(self.SCHEDULES)}, got {schedule!r}")
         _lib.check(self.lib.dd_set_schedule(self.handle, self.SCHEDULES[schedule]), self.lib)
+        self._schedule = schedule
 
     def gemm_mode(self) -> str:
         m = ctypes.c_int()
@@ -299,11 +318,16 @@ class InFlightPlanner:
     stream (its inputs)."""
 
     def __init__(self, config: Optional[TransfuserConfig] = None, state_dict: Optional[Mapping] = None,
-                 device: Optional[int] = None, gemm: Optional[str] = None, lanes: int = 2):
+                 device: Optional[int] = None, gemm: Optional[str] = None, lanes: int = 2,
+                 models: Optional[List[DiffusionDriveModel]] = None):
+        """``models``: existing handles to use as the lanes (e.g. ``[m] + [m.clone() for _ in ...]``) instead of
+        building ``lanes`` handles from ``state_dict``."""
+        if models is not None:
+            lanes = len(models)
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
-        self.lanes: List[DiffusionDriveModel] = [DiffusionDriveModel(config, state_dict, device, gemm)
-                                                 for _ in range(lanes)]
+        self.lanes: List[DiffusionDriveModel] = list(models) if models is not None else \
+            [DiffusionDriveModel(config, state_dict, device, gemm) for _ in range(lanes)]
         self.device = self.lanes[0].device
         if lanes > 1:
             for m in self.lanes:

@@ -15,10 +15,14 @@ the feature building and the forward batched on the GPU:
   PyTorch's 16-wide CPU normal fill aligned - tests/test_runner.py), so a seeded batched run equals a
   seeded per-token run scene for scene;
 * ``run_distributed`` shards the token list over the ranks of a torch.distributed group (one
-  process per GPU) and gathers the per-rank maps with one ``all_gather_object``.
+  process per GPU) and gathers the per-rank maps with one ``all_gather_object``;
+* ``lanes`` > 1 keeps that many batches in flight on the GPU (model.py InFlightPlanner: the agent's
+  handle plus clones, each a single-stream forward on a stream of its own); a batch is finished -
+  synchronised, its lane's numerics flag read - before its lane takes the next one.
 
 PDM scoring stays on the CPU (``pdm_score``, out of scope): feed it the returned trajectories.
 """
+import collections
 from typing import Callable, Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
@@ -29,11 +33,16 @@ from .features import TransfuserFeatureBuilder
 
 
 class BatchedTrajectoryRunner:
-    def __init__(self, agent: DiffusionDriveAgent, batch_size: int = 64, device: Optional[int] = None):
+    def __init__(self, agent: DiffusionDriveAgent, batch_size: int = 64, device: Optional[int] = None,
+                 lanes: int = 1):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
         self.agent = agent
         self.batch_size = batch_size
+        self.lanes = lanes
+        self._clones: List = []
         self.device = agent._transfuser_model.device if device is None else device
         self.builder = TransfuserFeatureBuilder(agent._config, device=self.device)
         self.failed: List[Tuple[str, str]] = []
@@ -47,33 +56,50 @@ class BatchedTrajectoryRunner:
 
     def _finish(self, job) -> Dict[str, Trajectory]:
         """Wait for a launched batch; if its forward raised a numerics flag, re-run it directly in fp32."""
-        tokens, feats, noise, out = job
-        model = self.agent._transfuser_model
+        tokens, feats, noise, out, model, stream = job
+        if stream is not None:
+            stream.synchronize()
         if model.numerics_flags(clear=True):
             with torch.no_grad():
                 out = model.rerun_fp32(feats, noise)
         poses = out["trajectory"].cpu().numpy()
         return {t: Trajectory(np.ascontiguousarray(poses[i])) for i, t in enumerate(tokens)}
 
-    def _run_batches(self, batches: Iterable[Tuple[List[str], List]]) -> Dict[str, Trajectory]:
-        """Software-pipelined: batch i+1's host-side feature staging (the raw-sensor copy into the pinned
-        stage) runs while batch i's forward is on the GPU; batch i is then finished (synchronised, its numerics
-        flag read - the feature kernels raise none) before batch i+1's forward is launched, so every flag
-        belongs to one forward."""
+    def _planner(self):
+        from .model import InFlightPlanner
         model = self.agent._transfuser_model
+        while len(self._clones) < self.lanes - 1:
+            self._clones.append(model.clone())
+        return InFlightPlanner(models=[model] + self._clones[:self.lanes - 1])
+
+    def _run_batches(self, batches: Iterable[Tuple[List[str], List]]) -> Dict[str, Trajectory]:
+        """Software-pipelined: the next batch's host-side feature staging (the raw-sensor copy into the pinned
+        stage) runs while up to ``lanes`` forwards are on the GPU; the oldest batch is finished (synchronised, its
+        lane's numerics flag read - the feature kernels raise none) before its lane takes another batch, so every
+        flag belongs to one forward."""
+        pl = self._planner()
+        for m in pl.lanes:
+            m.numerics_flags(clear=True)
+            if len(pl) > 1:
+                m.set_streams(1)
         out: Dict[str, Trajectory] = {}
-        prev = None
-        for tokens, inputs in batches:
-            feats, noise = self._features(inputs)
-            if prev is not None:
-                out.update(self._finish(prev))
-            else:
-                model.numerics_flags(clear=True)
-            with torch.no_grad():
-                res = model.forward(feats, noise=noise, safe=False)
-            prev = (tokens, feats, noise, res)
-        if prev is not None:
-            out.update(self._finish(prev))
+        pending = collections.deque()
+        try:
+            for tokens, inputs in batches:
+                feats, noise = self._features(inputs)
+                if len(pending) == len(pl):
+                    out.update(self._finish(pending.popleft()))
+                with torch.no_grad(), pl.next_lane() as m:
+                    s = pl.streams[pl.lanes.index(m)]
+                    res = m.forward(feats, noise=noise, safe=False,
+                                    stream=s if s is not None else None)
+                pending.append((tokens, feats, noise, res, m, s))
+            while pending:
+                out.update(self._finish(pending.popleft()))
+        finally:
+            if len(pl) > 1:
+                for m in pl.lanes:
+                    m.set_streams(2)
         return out
 
     def run(self, tokens: Iterable[str], get_agent_input: Callable[[str], object]) -> Dict[str, Trajectory]:

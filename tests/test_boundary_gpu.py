@@ -113,7 +113,7 @@ def test_flagged_forward_reruns_in_fp32(gpu_model):
         runner.agent = _Agent()
         res = gpu_model.forward(f, noise=nz)
         with pytest.warns(UserWarning):
-            got = runner._finish((["t0", "t1"], f, nz, res))
+            got = runner._finish((["t0", "t1"], f, nz, res, gpu_model, None))  # (tokens, feats, noise, out, lane, stream)
         assert np.array_equal(np.stack([got["t0"].poses, got["t1"].poses]), ref.cpu().numpy())
         assert gpu_model.numerics_flags() == 0
     finally:

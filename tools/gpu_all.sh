@@ -15,5 +15,5 @@ step tests 900 python -u -m pytest tests -v -m gpu -x -rf --timeout 300 --timeou
 step bench 600 python bench.py ${BENCH_ARGS:-}
 cd /tmp && export TMPDIR=/tmp
 # single-stream replays (DDMI_STREAMS=0) so per-kernel durations match bench.py's profiled replay; no fp32 leg
-DDMI_STREAMS=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof" -o run -- python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-compare > "$R/gpurun_out/prof.log" 2>&1
+DDMI_STREAMS=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof" -o run -- python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-compare --in-flight 1 > "$R/gpurun_out/prof.log" 2>&1
 rc=$?; echo "[rocprof] rc=$rc"; tail -2 "$R/gpurun_out/prof.log"; exit $rc
