@@ -23,6 +23,11 @@
 #include <set>
 #include <vector>
 
+#ifdef DDMI_SEGV_TRACE
+#define DD_TRACE(...) (fprintf(stderr, "[ddmi-trace] " __VA_ARGS__), fputc('\n', stderr), fflush(stderr))
+#else
+#define DD_TRACE(...) ((void)0)
+#endif
 #include "../../include/ddmi.h"
 #include "common.h"
 #include "decoder_mk.h"
@@ -1746,11 +1751,14 @@ class Model {
   void forward_chunk(const float* camera, const float* lidar, const float* status, const float* noise, int B,
                      int steps, const Outs& o, hipStream_t caller, uint64_t scene0) {
     DD_HIP_CHECK(hipSetDevice(device));
+    DD_TRACE("forward_chunk B=%d steps=%d caller=%p use_side=%d", B, steps, (void*)caller, (int)use_side);
     OnStream on(*this, caller);
     const bool heads = o.sem || o.ag_states || o.ag_labels;
     const uint64_t gen0 = generation;
     stage_inputs(camera, lidar, status, noise, B, scene0);
+    DD_TRACE("staged");
     ensure_film(steps);
+    DD_TRACE("film");
     if (generation != gen0) known_shapes.clear();
     const std::string key = std::to_string(B) + "/" + std::to_string(steps) + "/" + std::to_string(heads) + "/g" +
                             std::to_string(gemm_mode) + "/s" + std::to_string(schedule);
@@ -1761,6 +1769,7 @@ class Model {
         graph_gen = generation;
       }
       auto it = graphs.find(key);
+      DD_TRACE("graph key %s cached=%d", key.c_str(), (int)(it != graphs.end()));
       if (it == graphs.end()) {
         hipGraph_t g;
         hipGraphExec_t ex = nullptr;
@@ -1772,20 +1781,27 @@ class Model {
           (void)hipStreamEndCapture(st, &dummy);
           throw;
         }
+        DD_TRACE("captured");
         DD_HIP_CHECK(hipStreamEndCapture(st, &g));
+        DD_TRACE("end capture");
         DD_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+        DD_TRACE("instantiated");
         DD_HIP_CHECK(hipGraphDestroy(g));
         it = graphs.emplace(key, ex).first;
       }
       DD_HIP_CHECK(hipGraphLaunch(it->second, st));
+      DD_TRACE("launched");
     } else {
       // eager run (the first call for a shape allocates every buffer; later calls are captured)
       const uint64_t gen1 = generation;
+      DD_TRACE("eager");
       forward_body(B, steps, heads);
+      DD_TRACE("eager done");
       if (generation != gen1) known_shapes.clear();
       known_shapes.insert(key);
     }
     const int Q = cfg.num_modes, P = cfg.num_poses;
+    DD_TRACE("copy out");
     copy_out(o.traj, "trajectory", (size_t)B * P * 3);
     copy_out(o.modes, "poses_reg", (size_t)B * Q * P * 3);
     copy_out(o.cls, "poses_cls", (size_t)B * Q);
@@ -1812,6 +1828,23 @@ struct dd_handle {
 };
 
 static thread_local std::string g_last_error;
+
+#ifdef DDMI_SEGV_TRACE
+// diagnostic build only (DDMI_BUILD_VARIANT=dbg): a host backtrace on SIGSEGV (addr2line -e the library)
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
+static void ddmi_segv(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "[ddmi] SIGSEGV backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+__attribute__((constructor)) static void ddmi_segv_install() { signal(SIGSEGV, ddmi_segv); }
+#endif
 
 template <class F>
 static int guarded(F&& f) {
@@ -1872,6 +1905,9 @@ int dd_forward_ex(dd_handle* h, const float* camera, const float* lidar, const f
   return guarded([&] {
     if (!h || !outs) throw std::invalid_argument("dd_forward_ex: null handle/outputs");
     std::lock_guard<std::mutex> lk(h->mu);
+#ifdef DDMI_SEGV_TRACE
+    signal(SIGSEGV, ddmi_segv);  // the HSA runtime may have replaced it since the library loaded
+#endif
     Model::Outs o;
     o.traj = outs->trajectory;
     o.modes = outs->poses_reg;
