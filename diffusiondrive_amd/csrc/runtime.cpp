@@ -113,6 +113,35 @@ static void trunk_channels(int arch, int ch[5], bool& bottleneck) {
   }
 }
 
+// Process-wide pool of the handles' own streams: a destroyed handle returns its streams instead of destroying them,
+// and a new handle takes them back. Creating and destroying many streams in one process (handles of the parity
+// tests, batches-in-flight lanes and their clones) was followed by a host segfault inside hipGraphLaunch of a later
+// handle's two-stream graph (ROCm 7.2; reproduced by tests/test_runner.py + test_inflight_gpu.py + test_agent.py in
+// that order, the fault inside libamdhip64 under hipGraphLaunch).
+static std::mutex g_stream_pool_mu;
+static std::map<int, std::vector<hipStream_t>> g_stream_pool;
+
+static hipStream_t pooled_stream(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_stream_pool_mu);
+    auto& v = g_stream_pool[device];
+    if (!v.empty()) {
+      hipStream_t s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  DD_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return s;
+}
+
+static void release_stream(int device, hipStream_t s) {
+  (void)hipStreamSynchronize(s);
+  std::lock_guard<std::mutex> lk(g_stream_pool_mu);
+  g_stream_pool[device].push_back(s);
+}
+
 class Model {
  public:
   dd_config cfg;
@@ -225,8 +254,8 @@ class Model {
     }
     // default-priority streams: either one at the device's greatest priority measured 3-3.5 % slower
     // in the B = 64 bench graph, both at the least priority 33 % slower
-    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_main, hipStreamNonBlocking));
-    DD_HIP_CHECK(hipStreamCreateWithFlags(&st_side, hipStreamNonBlocking));
+    st_main = pooled_stream(device);
+    st_side = pooled_stream(device);
     st = st_own = st_main;
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
@@ -291,8 +320,8 @@ class Model {
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     for (auto& e : fj_ev) (void)hipEventDestroy(e);
-    if (st_main) (void)hipStreamDestroy(st_main);
-    if (st_side) (void)hipStreamDestroy(st_side);
+    if (st_main) release_stream(device, st_main);
+    if (st_side) release_stream(device, st_side);
     if (num_flags) (void)hipFree(num_flags);
     if (in_tab) (void)hipFree(in_tab);
     if (tf_mk_layers) (void)hipFree(tf_mk_layers);
