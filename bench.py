@@ -94,6 +94,8 @@ def parse():
     p.add_argument("--in-flight", type=int, default=3,
                    help="batches in flight per GPU (InFlightPlanner lanes: single-stream handles on streams of their "
                         "own); 1 = one two-stream forward at a time")
+    p.add_argument("--lane-streams", type=int, default=1, choices=[1, 2],
+                   help="streams of each lane's captured forward when --in-flight > 1")
     p.add_argument("--cpu-plumbing", action="store_true",
                    help="tests only: launcher + gloo all_gather + JSON with a stand-in step (no forward)")
     return p.parse_args()
@@ -154,7 +156,7 @@ def main():
     cfg = TransfuserConfig(image_architecture=args.arch)
     sd = seeded_state_dict(cfg, 0)
     # args.in_flight lanes (handles with the same weights); lane 0 also serves the profiled replay
-    pl = InFlightPlanner(cfg, sd, device=local, lanes=args.in_flight)
+    pl = InFlightPlanner(cfg, sd, device=local, lanes=args.in_flight, lane_streams=args.lane_streams)
     pl.set_gemm_mode(args.gemm)
     model = pl.lanes[0]
     B = args.batch
@@ -265,7 +267,7 @@ def main():
             one_at_a_time = {"value": round(B * n1 / dt1, 3), "ms_per_step": round(dt1 / n1 * 1e3, 3), "steps": n1,
                              "note": "in_flight 1: one two-stream forward at a time (its ms_per_step is the batch "
                                      "latency of that mode)"}
-            model.set_streams(1)
+            model.set_streams(args.lane_streams)
         # PCIe-inclusive: inputs staged from pinned host memory every step (one device buffer set per lane)
         host = {k: torch.from_numpy(inp[k]).pin_memory() for k in keys}
         host_nz = torch.from_numpy(inp["noise"]).pin_memory()

@@ -319,9 +319,10 @@ class InFlightPlanner:
 
     def __init__(self, config: Optional[TransfuserConfig] = None, state_dict: Optional[Mapping] = None,
                  device: Optional[int] = None, gemm: Optional[str] = None, lanes: int = 2,
-                 models: Optional[List[DiffusionDriveModel]] = None):
+                 models: Optional[List[DiffusionDriveModel]] = None, lane_streams: int = 1):
         """``models``: existing handles to use as the lanes (e.g. ``[m] + [m.clone() for _ in ...]``) instead of
-        building ``lanes`` handles from ``state_dict``."""
+        building ``lanes`` handles from ``state_dict``. ``lane_streams`` 2 keeps every lane's two-stream graph
+        (three streams per lane with the hand-off: worth it only with $GPU_MAX_HW_QUEUES raised above 4)."""
         if models is not None:
             lanes = len(models)
         if lanes < 1:
@@ -331,7 +332,7 @@ class InFlightPlanner:
         self.device = self.lanes[0].device
         if lanes > 1:
             for m in self.lanes:
-                m.set_streams(1)
+                m.set_streams(lane_streams)
         self.streams = [torch.cuda.Stream(torch.device(f"cuda:{self.device}")) for _ in range(lanes)] \
             if lanes > 1 else [None]
         self._next = 0
