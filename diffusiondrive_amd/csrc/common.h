@@ -230,7 +230,11 @@ __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], ch
         v.z = fmaxf(v.z, 0.f);
         v.w = fmaxf(v.w, 0.f);
       }
+#ifdef DDMI_EPI_NT  // experiment build (DDMI_BUILD_VARIANT=epint): nontemporal epilogue stores
+      __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(a.out + oo[k] + nq));
+#else
       *reinterpret_cast<f4_t*>(a.out + oo[k] + nq) = v;
+#endif
     }
   }
   return bad;

@@ -10,6 +10,6 @@ for v in "$@"; do
   rc=$?; echo "[$v tests] rc=$rc $(tail -1 gpurun_out/lab_$v.log)"; [ $rc -ne 0 ] && exit $rc
 done
 for l in libddmi.so $(for v in "$@"; do echo _variants/libddmi_$v.so; done) libddmi.so; do
-  DDMI_LIB=$PWD/diffusiondrive_amd/$l timeout -k 10 200 python bench.py --steps 60 --no-cpu-baseline --no-compare > gpurun_out/lab.log 2>&1 || { tail -5 gpurun_out/lab.log; exit 1; }
+  DDMI_LIB=$PWD/diffusiondrive_amd/$l timeout -k 10 200 python bench.py --steps ${ABSTEPS:-60} --no-cpu-baseline --no-compare ${BENCH_ARGS:-} > gpurun_out/lab.log 2>&1 || { tail -5 gpurun_out/lab.log; exit 1; }
   python -c "import json;d=json.loads(open('gpurun_out/lab.log').read().strip().splitlines()[-1]);dm=d['device_ms_per_step'];print('$l', d['value'], d['ms_per_step'], {k: dm[k] for k in ('conv_x6','conv_x5','conv_x3','attn','stem_pool','bilinear')})"
 done
