@@ -128,3 +128,21 @@ def test_model_requires_gpu_loudly():
     from diffusiondrive_amd.model import DiffusionDriveModel
     with pytest.raises(_lib.DDMIUnavailable):
         DiffusionDriveModel()
+
+
+def test_inflight_and_runner_lane_counts_validated_before_gpu_work():
+    """Batches-in-flight arguments: lanes < 1 is rejected before any handle is built; dd_set_streams validates its
+    handle and count through the ABI."""
+    import ctypes
+    from diffusiondrive_amd import _lib
+    from diffusiondrive_amd.model import InFlightPlanner
+    from diffusiondrive_amd.runner import BatchedTrajectoryRunner
+    with pytest.raises(ValueError):
+        InFlightPlanner(lanes=0)
+    with pytest.raises(ValueError):
+        InFlightPlanner(models=[])
+    with pytest.raises(ValueError):
+        BatchedTrajectoryRunner(None, lanes=0)
+    lib = _lib.load()
+    assert lib.dd_set_streams(None, 1) == -1 and b"null" in lib.dd_last_error()
+    assert lib.dd_set_streams(ctypes.c_void_p(0), 2) == -1
