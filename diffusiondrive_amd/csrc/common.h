@@ -230,11 +230,10 @@ __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], ch
         v.z = fmaxf(v.z, 0.f);
         v.w = fmaxf(v.w, 0.f);
       }
-#ifdef DDMI_EPI_NT  // experiment build (DDMI_BUILD_VARIANT=epint): nontemporal epilogue stores
+      // nontemporal: with conv_x6's and the upsample-add's output stores the same, +0.5 % scenes/s same-box in both
+      // the in-flight and the one-at-a-time bench (profiles/round3_o_nt_stores_ab.txt); conv_x5 / conv_x3 shapes
+      // alone 1-10 % faster on the conv micro-benchmark
       __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(a.out + oo[k] + nq));
-#else
-      *reinterpret_cast<f4_t*>(a.out + oo[k] + nq) = v;
-#endif
     }
   }
   return bad;

@@ -231,12 +231,9 @@ __global__ __launch_bounds__(256) void bilinear_add4_kernel(View4 in, int Hi, in
     v.y = p[u].y + v.y;
     v.z = p[u].z + v.z;
     v.w = p[u].w + v.w;
-#ifdef DDMI_NT_ALL  // experiment build (DDMI_BUILD_VARIANT=ntall): nontemporal output stores
+    // nontemporal output store (common.h epi_quads: +0.5 % scenes/s with all three sites)
     typedef float ntf4 __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store((ntf4){v.x, v.y, v.z, v.w}, reinterpret_cast<ntf4*>(obase + (int64_t)x * out.sw + c));
-#else
-    *reinterpret_cast<float4*>(obase + (int64_t)x * out.sw + c) = v;
-#endif
   }
 }
 
