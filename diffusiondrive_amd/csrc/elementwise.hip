@@ -384,7 +384,12 @@ __global__ __launch_bounds__(256) void layernorm_v4_kernel(const float* __restri
       o.z = o.z * (1.f + a.z) + c.z;
       o.w = o.w * (1.f + a.w) + c.w;
     }
+#ifdef DDMI_NT2  // experiment build (DDMI_BUILD_VARIANT=nt2): nontemporal LayerNorm output stores
+    typedef float ntf4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store((ntf4){o.x, o.y, o.z, o.w}, reinterpret_cast<ntf4*>(yr + c4));
+#else
     yr[c4] = o;
+#endif
   }
 }
 

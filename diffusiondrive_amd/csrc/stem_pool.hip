@@ -235,7 +235,11 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
           mx.z = fmaxf(mx.z, v.z);
           mx.w = fmaxf(mx.w, v.w);
         }
+#ifdef DDMI_NT2  // experiment build (DDMI_BUILD_VARIANT=nt2): nontemporal pooled-map stores
+      if (gy < Hp && gx < Wp) __builtin_nontemporal_store(mx, reinterpret_cast<sp_f4*>(out + (((int64_t)b * Hp + gy) * Wp + gx) * 64 + 4 * q));
+#else
       if (gy < Hp && gx < Wp) *reinterpret_cast<sp_f4*>(out + (((int64_t)b * Hp + gy) * Wp + gx) * 64 + 4 * q) = mx;
+#endif
     }
     __syncthreads();  // the next tile overwrites the patch and the stem tile
   }
