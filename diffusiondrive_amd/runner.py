@@ -90,9 +90,8 @@ class BatchedTrajectoryRunner:
                 if len(pending) == len(pl):
                     out.update(self._finish(pending.popleft()))
                 with torch.no_grad(), pl.next_lane() as m:
-                    s = pl.streams[pl.lanes.index(m)]
-                    res = m.forward(feats, noise=noise, safe=False,
-                                    stream=s if s is not None else None)
+                    s = torch.cuda.current_stream(m.device)  # the lane's stream (the caller's with one lane)
+                    res = m.forward(feats, noise=noise, safe=False, stream=s)
                 pending.append((tokens, feats, noise, res, m, s))
             while pending:
                 out.update(self._finish(pending.popleft()))
