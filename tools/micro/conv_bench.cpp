@@ -40,6 +40,8 @@ static const Shape kShapes[] = {
     {"img.l2.s2", 64, 64, 256, 64, 128, 3, 2, 0},
     {"img.stem7", 64, 256, 1024, 4, 64, 7, 2, 0},
     {"gpt.mlp0", 64 * 320, 1, 1, 512, 2048, 1, 1, 0},
+    {"gpt.mlp0.h", 16 * 256, 1, 1, 512, 2048, 1, 1, 0},   // 128 tiles: half the chip (shared-bandwidth probe)
+    {"gpt.mlp0.q", 8 * 256, 1, 1, 512, 2048, 1, 1, 0},    // 64 tiles: a quarter
     {"gpt.qkv4", 64 * 320, 1, 1, 512, 1536, 1, 1, 0},
     {"gpt.mlp2", 64 * 320, 1, 1, 2048, 512, 1, 1, 1},
     {"gpt.proj4", 64 * 320, 1, 1, 512, 512, 1, 1, 1},
