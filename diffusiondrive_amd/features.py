@@ -102,8 +102,8 @@ def _upload_chunked(dev: torch.device, kind: str, host: torch.Tensor, shape, ite
     if cs is None:
         cs = _copy_streams[dev.index] = torch.cuda.Stream(device=dev)
     cur = torch.cuda.current_stream(dev)
-    d = torch.empty(tuple(shape), dtype=host.dtype, device=dev)
-    cs.wait_stream(cur)  # d's memory is free on the copy stream too
+    with torch.cuda.stream(cs):  # allocated for the copy stream (no wait on the caller's queued work)
+        d = torch.empty(tuple(shape), dtype=host.dtype, device=dev)
     flat_h, flat_d = host.view(items, -1), d.view(items, -1)
     per = -(-items // groups)
     pool = _copy_pool()
@@ -115,7 +115,7 @@ def _upload_chunked(dev: torch.device, kind: str, host: torch.Tensor, shape, ite
     ev = torch.cuda.Event()
     ev.record(cs)
     cur.wait_event(ev)
-    d.record_stream(cs)
+    d.record_stream(cur)
     _stages[(dev.index, kind)][1] = ev
     return d
 
