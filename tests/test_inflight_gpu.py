@@ -89,3 +89,21 @@ def test_set_streams_rejects_bad_count(gpu_model):
     with pytest.raises(_lib.DDMIError):
         gpu_model.set_streams(3)
     assert np.isfinite(gpu_model.forward(*_inputs(1, 3)[:1], noise=_inputs(1, 3)[1])["trajectory"].cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("gemm", ["fp32", "bf16"])
+def test_inflight_lanes_in_other_gemm_modes(seeded_sd, gemm):
+    """The lanes in the fp32 and bf16 gemm modes (other kernel families on the caller's stream): each batch equals a
+    single-stream handle of the same mode bit for bit."""
+    pl = InFlightPlanner(state_dict=seeded_sd, device=0, lanes=2, gemm=gemm)
+    solo = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm=gemm)
+    try:
+        solo.set_streams(1)
+        batches = [_inputs(2, 200 + i) for i in range(4)]
+        outs = [pl.forward(f, noise=nz)["trajectory"] for f, nz in batches]
+        pl.synchronize()
+        for i, (f, nz) in enumerate(batches):
+            assert torch.equal(outs[i].cpu(), solo.forward(f, noise=nz)["trajectory"].cpu()), (gemm, i)
+    finally:
+        pl.close()
+        solo.close()
