@@ -224,6 +224,9 @@ def main():
 
     # ---- roofline of the dominant kernel: a profiled single-stream replay of the same workload
     # (HIP events around every launch on the stream it is issued to)
+    # (lane 0 as the two-stream handle of the one-at-a-time mode: the profiled replay is single-stream either way, and
+    # its value_proj takes the K split a two-stream handle uses - a single-stream lane runs it unsplit)
+    model.set_streams(2)
     model.set_profiling(True)
     model.reset_stats()
     prof_steps = max(1, min(args.steps, 5))
@@ -237,6 +240,7 @@ def main():
     value_proj = value_proj_record(model, other["value_proj"], prof_steps, B, args)
     other.update({k: v for k, v in conv_stats.items() if k != main_k})
     model.set_profiling(False)
+    model.set_streams(args.lane_streams if args.in_flight > 1 else 2)
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["flops"] / max(st["launches"], 1)
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0

@@ -111,8 +111,9 @@ int dd_set_graph(dd_handle* h, int enable);
  * tf decoder and the optional heads on a second stream beside the rest; 1 = everything in order on one stream,
  * and a forward called on a non-default stream runs on that stream itself (no hand-off through the handle's
  * own stream). The batches-in-flight mode: N single-stream handles driven from N caller streams keep N forwards
- * in flight on one device, one hardware queue each (diffusiondrive_amd/model.py InFlightPlanner). No reference
- * counterpart (the reference runs one eager forward at a time). */
+ * in flight on one device, one hardware queue each (diffusiondrive_amd/model.py InFlightPlanner); such a handle runs
+ * the decoder's value_proj without its K split (less work on a shared device; $DDMI_VPROJ_SPLITS overrides). No
+ * reference counterpart (the reference runs one eager forward at a time). */
 int dd_set_streams(dd_handle* h, int n);
 /* GEMM arithmetic of every conv / linear of the path:
  *   DD_GEMM_FP32   fp32-input MFMA (v_mfma_f32_32x32x2_f32), an exact fp32 fma chain;
