@@ -15,9 +15,14 @@ A step = one forward of B synthetic scenes resident in HBM (+ the all_gather whe
 (default 3) keeps L steps in flight per GPU (diffusiondrive_amd/model.py InFlightPlanner); the timed region
 still brackets all K steps completely.
 Rank 0 prints ONE JSON line. Besides the contract fields it reports:
-  * ``median_ms_per_step``: median interval between consecutive step completions (HIP events on the lanes'
-    streams); ``median_batch_latency_ms``: median start -> end of one step's forward on its lane (with
-    ``--in-flight N`` > 1, N batches share the device, so a batch takes longer while the steps complete faster);
+  * ``median_ms_per_step``: median step interval from the completion events (HIP events on the lanes' streams,
+    end times sorted on the device clock, windows of ``in_flight`` completions: ``completion_intervals``);
+    ``median_batch_latency_ms``: median start -> end of one step's forward on its lane (with ``--in-flight N`` > 1,
+    N batches share the device, so a batch takes longer while the steps complete faster); ``scenes_resident`` =
+    batch x in_flight;
+  * ``in_flight_1``: the same workload one batch at a time - the strict "scenes/s at batch 64" figure;
+  * ``gather_check``: every rank's slice of the all_gather output equals its own forward (N > 1: the C3 workload,
+    shards of one seeded global batch), and shard 0's waypoint L2 against the reference golden;
   * ``fp32_leg``: the same workload on the fp32-MFMA path (N = 1), the conservative headline;
   * ``h2d_included``: the same forward with its inputs copied from pinned host memory every
     step (PCIe-inclusive; never ``value``);
@@ -148,7 +153,7 @@ def main():
     from diffusiondrive_amd.config import TransfuserConfig
     from diffusiondrive_amd.dist import ScenePlanner
     from diffusiondrive_amd.model import InFlightPlanner
-    from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
+    from diffusiondrive_amd.weights import reference_noise, seeded_state_dict, synthetic_inputs
 
     if args.in_flight < 1:
         print("[bench] --in-flight must be >= 1", file=sys.stderr)
@@ -160,12 +165,19 @@ def main():
     pl.set_gemm_mode(args.gemm)
     model = pl.lanes[0]
     B = args.batch
+    # this rank's shard of ONE seeded global batch (config C3 at N = 8): scenes of rank r are
+    # synthetic_inputs(B, 1234 + r), and the DDIM start noise is drawn once for all B * world scenes
+    # (torch.manual_seed(1234); torch.randn(B * world, 20, 8, 2)) and sliced - tests/test_sharding_gpu.py's global
+    # batch. Shard 0 is the reference golden's batch (tests/golden/ref_b64_s1234.npz).
     inp = synthetic_inputs(B, 1234 + rank, cfg)
+    inp["noise"] = np.ascontiguousarray(reference_noise(B * world, 1234, cfg)[rank * B:(rank + 1) * B])
     keys = ("camera_feature", "lidar_feature", "status_feature")
     feats = {k: torch.from_numpy(inp[k]).to(dev) for k in keys}
     noise = torch.from_numpy(inp["noise"]).to(dev)
     planner = ScenePlanner(lambda f, nz: pl.forward(f, noise=nz, steps=args.denoise_steps)["trajectory"])
     marks = []  # per step: (start, end) HIP events on the stream the step ran on
+
+    last_local = [None]  # this rank's own trajectories of the latest step (checked against its gathered slice)
 
     def lane_step(body):
         # the next lane: its forward and the all_gather of its trajectories on the lane's stream
@@ -173,16 +185,18 @@ def main():
             s = torch.cuda.current_stream(dev)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            o = planner.gather(body(m, s))
+            local_traj = body(m, s)
+            o = planner.gather(local_traj)
             e1.record(s)
             marks.append((e0, e1))
+            last_local[0] = local_traj
             return o
 
     def step():
         # per-rank shard of the global batch (weak scaling) + one RCCL all_gather of trajectories
         return lane_step(lambda m, s: m.forward(feats, noise=noise, steps=args.denoise_steps, stream=s)["trajectory"])
 
-    def timed(fn, k):
+    def timed(fn, k, lanes=args.in_flight):
         """k steps between barrier + synchronize. Per step: the interval between consecutive step completions
         (HIP events on the lanes' streams, one device clock) and the batch latency (its own start -> end)."""
         if dist is not None:
@@ -199,10 +213,7 @@ def main():
         if dist is not None:
             dist.barrier()
         el = time.perf_counter() - t0
-        ends = [e_start] + [e1 for _, e1 in marks]
-        per = [ends[i].elapsed_time(ends[i + 1]) for i in range(len(ends) - 1)]
-        lat = [e0.elapsed_time(e1) for e0, e1 in marks]
-        return o, el, per, lat
+        return o, el, completion_intervals(e_start, marks, lanes), [e0.elapsed_time(e1) for e0, e1 in marks]
 
     for _ in range(args.warmup):
         out = step()
@@ -216,7 +227,17 @@ def main():
         elapsed, med, lat_med = float(t[0].item()), float(t[1].item()), float(t[2].item())
     ms_per_step = elapsed / args.steps * 1e3
     scenes_per_s = B * world * args.steps / elapsed
+    torch.cuda.synchronize()
     traj_gpu = out[rank * B:(rank + 1) * B].detach().cpu().numpy()
+    # the gathered tensor holds every rank's shard in rank order: each rank checks its own slice against the
+    # trajectories it computed (bit for bit), and the ranks agree on the result (MIN over ranks)
+    gather_ok = bool(np.array_equal(traj_gpu, last_local[0].detach().cpu().numpy()))
+    gathered = out.detach().cpu().numpy()
+    if dist is not None:
+        t = torch.tensor([1 if gather_ok else 0], device=dev, dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        gather_ok = bool(t.item())
+    shard0_golden_l2 = golden_l2(gathered, args.arch, B, args.denoise_steps) if B == 64 else None
     num_flags = pl.numerics_flags()
     if num_flags:
         print(f"[bench] WARNING: numerics flags {num_flags:#x} raised (f16x3 overflow): result untrustworthy",
@@ -267,7 +288,8 @@ def main():
             for _ in range(3):
                 model.forward(feats, noise=noise, steps=args.denoise_steps)
             n1 = max(5, min(args.steps // 2, 60))
-            _, dt1, _, _ = timed(lambda: model.forward(feats, noise=noise, steps=args.denoise_steps)["trajectory"], n1)
+            _, dt1, _, _ = timed(lambda: model.forward(feats, noise=noise, steps=args.denoise_steps)["trajectory"], n1,
+                                 lanes=1)
             one_at_a_time = {"value": round(B * n1 / dt1, 3), "ms_per_step": round(dt1 / n1 * 1e3, 3), "steps": n1,
                              "note": "in_flight 1: one two-stream forward at a time (its ms_per_step is the batch "
                                      "latency of that mode)"}
@@ -394,6 +416,12 @@ def main():
         },
         "decoder_cross_attention": value_proj,
         "numerics_flags": num_flags,
+        "scenes_resident": B * args.in_flight,
+        "gather_check": {"gathered_rows": int(gathered.shape[0]), "every_rank_slice_equals_local": gather_ok,
+                         "shard0_waypoint_l2_vs_golden": shard0_golden_l2,
+                         "note": "each rank's slice of the all_gather output equals its own forward bit for bit "
+                                 "(MIN over ranks); shard 0 = scenes 0..63 of the seeded global batch vs the "
+                                 "reference golden tests/golden/ref_b64_s1234.npz"},
     }
     if h2d is not None:
         result["h2d_included"] = h2d
@@ -440,6 +468,31 @@ def value_proj_record(model, vp, prof_steps, B, args):
             "live_mfma_equiv_util": round(live_tf * 3 / F16_MFMA_SUSTAINED_TFLOPS, 4),
             "note": "live_mfma_equiv_util = live-row f16 MFMA FLOP rate (3 products per MAC) / the measured sustained "
                     "whole-chip f16 MFMA rate; the PMC MFMA-busy of the same launches is in profiles/"}
+
+
+def completion_intervals(e_start, marks, lanes):
+    """Per-step intervals of a timed run from its step-completion events (``marks``: (start, end) HIP events, one
+    pair per step, recorded on the stream each step ran on). With several lanes the completions need not arrive in
+    issue order, so the end times are read against one start event on the device clock and SORTED; the interval is
+    then taken over a window of ``lanes`` consecutive completions ((c[i + L] - c[i]) / L), which is the steady-state
+    step time whether the lanes finish evenly staggered or in bursts. One lane: consecutive differences."""
+    ends = sorted(e_start.elapsed_time(e1) for _, e1 in marks)
+    L = max(1, min(int(lanes), len(ends) - 1))
+    if len(ends) < 2:
+        return [ends[0]] if ends else [0.0]
+    return [(ends[i + L] - ends[i]) / L for i in range(len(ends) - L)]
+
+
+def golden_l2(traj, arch, batch, steps):
+    """Waypoint L2 of the first 64 scenes of ``traj`` against the committed reference golden of that batch
+    (tests/golden/ref_b64_s1234.npz: the reference model's own output on seeded weights 0 and bench.py's rank-0 /
+    global-batch-shard-0 inputs and noise), or None when the run is not that workload."""
+    path = os.path.join(ROOT, "tests", "golden", "ref_b64_s1234.npz")
+    if arch != "resnet34" or steps != 2 or len(traj) < 64 or not os.path.exists(path):
+        return None
+    with np.load(path, allow_pickle=False) as z:
+        ref = z["trajectory"]
+    return waypoint_l2(np.asarray(traj)[:64], ref)
 
 
 def waypoint_l2(a, b):

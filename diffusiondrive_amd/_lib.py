@@ -58,6 +58,7 @@ _SIGS = {
     "dd_set_seed_at": (ctypes.c_int, [c_void_p, ctypes.c_ulonglong, ctypes.c_ulonglong]),
     "dd_set_graph": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_set_streams": (ctypes.c_int, [c_void_p, ctypes.c_int]),
+    "dd_get_streams": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "dd_set_gemm_mode": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_set_schedule": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_get_gemm_mode": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int)]),

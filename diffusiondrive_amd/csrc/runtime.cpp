@@ -121,8 +121,16 @@ static void trunk_channels(int arch, int ch[5], bool& bottleneck) {
 static std::mutex g_stream_pool_mu;
 static std::map<int, std::vector<hipStream_t>> g_stream_pool;
 
+static bool stream_pool_on() {
+  static const bool on = [] {
+    const char* e = getenv("DDMI_STREAM_POOL");  // 0: create / destroy per handle (the reproducer's A/B)
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static hipStream_t pooled_stream(int device) {
-  {
+  if (stream_pool_on()) {
     std::lock_guard<std::mutex> lk(g_stream_pool_mu);
     auto& v = g_stream_pool[device];
     if (!v.empty()) {
@@ -138,6 +146,10 @@ static hipStream_t pooled_stream(int device) {
 
 static void release_stream(int device, hipStream_t s) {
   (void)hipStreamSynchronize(s);
+  if (!stream_pool_on()) {
+    (void)hipStreamDestroy(s);
+    return;
+  }
   std::lock_guard<std::mutex> lk(g_stream_pool_mu);
   g_stream_pool[device].push_back(s);
 }
@@ -269,7 +281,8 @@ class Model {
     }
     if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
-    DD_HIP_CHECK(hipMemset(in_tab, 0, 4 * sizeof(float*)));
+    // zeroed on the handle's own stream and waited for: ordered before any forward, on whichever stream it runs
+    DD_HIP_CHECK(hipMemsetAsync(in_tab, 0, 4 * sizeof(float*), st_own));
     if (const char* e = getenv("DDMI_BEVPROJ")) {
       if (!strcmp(e, "fused")) bevproj_mode = 2;
       else if (!strcmp(e, "lowres")) bevproj_mode = 1;
@@ -286,7 +299,8 @@ class Model {
       if (max_chunk < 1 || max_chunk > 256) throw std::invalid_argument("DDMI_MAX_CHUNK must be in [1, 256]");
     }
     DD_HIP_CHECK(hipMalloc(&num_flags, sizeof(unsigned)));
-    DD_HIP_CHECK(hipMemset(num_flags, 0, sizeof(unsigned)));
+    DD_HIP_CHECK(hipMemsetAsync(num_flags, 0, sizeof(unsigned), st_own));
+    DD_HIP_CHECK(hipStreamSynchronize(st_own));
     if (const char* g = getenv("DDMI_GEMM")) {
       if (!strcmp(g, "fp32")) gemm_mode = DD_GEMM_FP32;
       else if (!strcmp(g, "f16x3")) gemm_mode = DD_GEMM_F16X3;
@@ -1799,6 +1813,8 @@ class Model {
                             std::to_string(gemm_mode) + "/s" + std::to_string(schedule);
     if (use_graph && !profiling && known_shapes.count(key)) {
       if (graph_gen != generation || graphs.size() > 8) {
+        // an earlier replay may still run (on the caller's stream in direct mode): ev_out marks the last forward
+        DD_HIP_CHECK(hipEventSynchronize(ev_out));
         for (auto& g : graphs) DD_HIP_CHECK(hipGraphExecDestroy(g.second));
         graphs.clear();
         graph_gen = generation;
@@ -1971,6 +1987,7 @@ int dd_destroy(dd_handle* h) {
 int dd_set_profiling(dd_handle* h, int enable) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->m->profiling = enable != 0;
   });
 }
@@ -1979,7 +1996,9 @@ int dd_set_streams(dd_handle* h, int n) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
     if (n != 1 && n != 2) throw std::invalid_argument("dd_set_streams: n must be 1 or 2");
+    std::lock_guard<std::mutex> lk(h->mu);  // a forward on another thread may be replaying a cached exec
     Model& m = *h->m;
+    DD_HIP_CHECK(hipSetDevice(m.device));
     if (m.use_side == (n == 2)) return;
     DD_HIP_CHECK(hipStreamSynchronize(m.st));
     DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a graph replayed on a caller's stream may still run
@@ -1989,9 +2008,18 @@ int dd_set_streams(dd_handle* h, int n) {
   });
 }
 
+int dd_get_streams(dd_handle* h, int* n) {
+  return guarded([&] {
+    if (!h || !n) throw std::invalid_argument("null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *n = h->m->use_side ? 2 : 1;
+  });
+}
+
 int dd_set_graph(dd_handle* h, int enable) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->m->use_graph = enable != 0;
   });
 }
@@ -2033,8 +2061,8 @@ int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear) {
     DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a single-stream forward may have run on the caller's stream
     DD_HIP_CHECK(hipMemcpy(flags, m.num_flags, sizeof(unsigned), hipMemcpyDeviceToHost));
     if (clear) {
-      DD_HIP_CHECK(hipMemset(m.num_flags, 0, sizeof(unsigned)));
-      DD_HIP_CHECK(hipStreamSynchronize(nullptr));  // cleared before any later forward's kernels run
+      DD_HIP_CHECK(hipMemsetAsync(m.num_flags, 0, sizeof(unsigned), m.st_own));
+      DD_HIP_CHECK(hipStreamSynchronize(m.st_own));  // cleared before any later forward's kernels run
     }
   });
 }
@@ -2042,6 +2070,7 @@ int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear) {
 int dd_reset_stats(dd_handle* h) {
   return guarded([&] {
     if (!h) throw std::invalid_argument("null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->m->collect();
     h->m->stats.clear();
   });
@@ -2050,6 +2079,7 @@ int dd_reset_stats(dd_handle* h) {
 int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long long* launches, double* flops) {
   return guarded([&] {
     if (!h || !kernel) throw std::invalid_argument("null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->m->collect();
     auto it = h->m->stats.find(kernel);
     ddmi::KStat s;
@@ -2063,6 +2093,7 @@ int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long lon
 int dd_kernel_bytes(dd_handle* h, const char* kernel, double* bytes) {
   return guarded([&] {
     if (!h || !kernel || !bytes) throw std::invalid_argument("null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->m->collect();
     auto it = h->m->stats.find(kernel);
     *bytes = it != h->m->stats.end() ? it->second.bytes : 0.0;
@@ -2083,6 +2114,7 @@ int dd_set_seed_at(dd_handle* h, unsigned long long seed, unsigned long long fir
 int dd_tap(dd_handle* h, const char* name, float* dst, size_t count, size_t* actual, void* stream) {
   return guarded([&] {
     if (!h || !name) throw std::invalid_argument("null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
     Model& m = *h->m;
     float* src = nullptr;
     size_t n = 0;

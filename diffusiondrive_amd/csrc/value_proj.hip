@@ -306,9 +306,18 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
+    // the sc1 / drained / one-adder / sc1-load form above is the measured hand-off of MI355X_MICROARCH.md's table
+    // (row 1); the agent-scope release before the add and the acquire after it make the ordering the memory
+    // model's, not the cache-policy bits' (one each per workgroup; the compiler-hazard wait after the release)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(a.tile_cnt + mt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     g_last = old == (unsigned)(S - 1);
-    if (old == (unsigned)(S - 1)) __hip_atomic_store(a.tile_cnt + mt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)(S - 1)) {
+      __hip_atomic_store(a.tile_cnt + mt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   if (!g_last) return;

@@ -212,6 +212,12 @@ class DiffusionDriveModel:
             nz = self._dev(noise)
             if tuple(nz.shape) != (B, Q, P, 2):
                 raise ValueError(f"noise must be (B,{Q},{P},2), got {tuple(nz.shape)}")
+        # the graph reads the camera / LiDAR planes in place (through the handle's input table) and copies status /
+        # noise on stream s: a caller that drops its tensors right after forward() returns must not have their
+        # memory handed to other work while s still reads it (tensors allocated on another stream)
+        for t in (cam, lid, st, nz):
+            if t is not None:
+                t.record_stream(s)
         dev = cam.device
         traj = torch.empty((B, P, 3), device=dev)
         outs = _lib.DDOutputs()
@@ -291,6 +297,12 @@ class DiffusionDriveModel:
         second stream; 1: one stream, and a forward called on a non-default stream runs on that stream itself
         (dd_set_streams; the per-lane mode of InFlightPlanner)."""
         _lib.check(self.lib.dd_set_streams(self.handle, int(n)), self.lib)
+
+    def stream_count(self) -> int:
+        """The handle's current stream count (1 or 2; dd_get_streams)."""
+        n = ctypes.c_int()
+        _lib.check(self.lib.dd_get_streams(self.handle, ctypes.byref(n)), self.lib)
+        return n.value
 
     def reset_stats(self):
         _lib.check(self.lib.dd_reset_stats(self.handle), self.lib)

@@ -18,7 +18,11 @@ the feature building and the forward batched on the GPU:
   process per GPU) and gathers the per-rank maps with one ``all_gather_object``;
 * ``lanes`` > 1 keeps that many batches in flight on the GPU (model.py InFlightPlanner: the agent's
   handle plus clones, each a single-stream forward on a stream of its own); a batch is finished -
-  synchronised, its lane's numerics flag read - before its lane takes the next one.
+  synchronised, its lane's numerics flag read - before its lane takes the next one;
+* failures are isolated per batch, as the reference isolates them per token (``run_pdm_score.py:77-100``:
+  any exception marks the token invalid and the loop goes on): an exception while building a batch's
+  features, launching its forward or finishing it marks that batch's tokens failed (``self.failed``)
+  and the other batches - those already in flight on other lanes included - complete.
 
 PDM scoring stays on the CPU (``pdm_score``, out of scope): feed it the returned trajectories.
 """
@@ -72,33 +76,66 @@ class BatchedTrajectoryRunner:
             self._clones.append(model.clone())
         return InFlightPlanner(models=[model] + self._clones[:self.lanes - 1])
 
+    def close(self):
+        """Release the lane clones' handles (the agent's own handle stays with the agent)."""
+        for m in self._clones:
+            m.close()
+        self._clones = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def _fail(self, tokens: List[str], err: BaseException):
+        self.failed.extend((t, repr(err)) for t in tokens)
+
     def _run_batches(self, batches: Iterable[Tuple[List[str], List]]) -> Dict[str, Trajectory]:
         """Software-pipelined: the next batch's host-side feature staging (the raw-sensor copy into the pinned
         stage) runs while up to ``lanes`` forwards are on the GPU; the oldest batch is finished (synchronised, its
         lane's numerics flag read - the feature kernels raise none) before its lane takes another batch, so every
-        flag belongs to one forward."""
+        flag belongs to one forward. An exception in one batch's features, launch or finish fails that batch's
+        tokens only."""
         pl = self._planner()
+        # every lane runs single-stream while several are in flight; each handle's own count is restored after
+        saved = [m.stream_count() for m in pl.lanes] if len(pl) > 1 else []
         for m in pl.lanes:
             m.numerics_flags(clear=True)
             if len(pl) > 1:
                 m.set_streams(1)
         out: Dict[str, Trajectory] = {}
         pending = collections.deque()
+
+        def finish_oldest():
+            job = pending.popleft()
+            try:
+                out.update(self._finish(job))
+            except Exception as e:  # noqa: BLE001 - per-batch isolation (run_pdm_score.py:77-100)
+                self._fail(job[0], e)
+
         try:
             for tokens, inputs in batches:
-                feats, noise = self._features(inputs)
+                try:
+                    feats, noise = self._features(inputs)
+                except Exception as e:  # noqa: BLE001
+                    self._fail(tokens, e)
+                    continue
                 if len(pending) == len(pl):
-                    out.update(self._finish(pending.popleft()))
-                with torch.no_grad(), pl.next_lane() as m:
-                    s = torch.cuda.current_stream(m.device)  # the lane's stream (the caller's with one lane)
-                    res = m.forward(feats, noise=noise, safe=False, stream=s)
+                    finish_oldest()
+                try:
+                    with torch.no_grad(), pl.next_lane() as m:
+                        s = torch.cuda.current_stream(m.device)  # the lane's stream (the caller's with one lane)
+                        res = m.forward(feats, noise=noise, safe=False, stream=s)
+                except Exception as e:  # noqa: BLE001
+                    self._fail(tokens, e)
+                    continue
                 pending.append((tokens, feats, noise, res, m, s))
             while pending:
-                out.update(self._finish(pending.popleft()))
+                finish_oldest()
         finally:
-            if len(pl) > 1:
-                for m in pl.lanes:
-                    m.set_streams(2)
+            for m, n in zip(pl.lanes, saved):
+                m.set_streams(n)
         return out
 
     def run(self, tokens: Iterable[str], get_agent_input: Callable[[str], object]) -> Dict[str, Trajectory]:

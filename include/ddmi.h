@@ -115,6 +115,9 @@ int dd_set_graph(dd_handle* h, int enable);
  * the decoder's value_proj without its K split (less work on a shared device; $DDMI_VPROJ_SPLITS overrides). No
  * reference counterpart (the reference runs one eager forward at a time). */
 int dd_set_streams(dd_handle* h, int n);
+/* The handle's current stream count (1 or 2, as dd_set_streams sets it): lets a caller that switches a handle to
+ * single-stream for batches in flight restore what it found (diffusiondrive_amd/runner.py). */
+int dd_get_streams(dd_handle* h, int* n);
 /* GEMM arithmetic of every conv / linear of the path:
  *   DD_GEMM_FP32   fp32-input MFMA (v_mfma_f32_32x32x2_f32), an exact fp32 fma chain;
  *   DD_GEMM_F16X3  3-product fp16 split on f16 MFMA (conv_x3.hip): each fp32 operand becomes

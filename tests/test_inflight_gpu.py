@@ -107,3 +107,71 @@ def test_inflight_lanes_in_other_gemm_modes(seeded_sd, gemm):
     finally:
         pl.close()
         solo.close()
+
+
+def test_inflight_inputs_dropped_right_after_forward(seeded_sd):
+    """The lanes read the caller's camera / LiDAR planes in place during the replay. A caller that drops its input
+    tensors right after pl.forward() returns and allocates on its own (default) stream must not get that memory
+    while a lane still reads it (model.py records the lane stream on the inputs): overwritten inputs would change the
+    trajectories."""
+    pl = InFlightPlanner(state_dict=seeded_sd, device=0, lanes=2)
+    solo = DiffusionDriveModel(state_dict=seeded_sd, device=0)
+    try:
+        solo.set_streams(1)
+        seeds = [300 + i for i in range(6)]
+        ref = []
+        for sd_ in seeds:
+            f, nz = _inputs(8, sd_)
+            ref.append(solo.forward(f, noise=nz)["trajectory"].cpu())
+        for _ in range(2):  # eager + capture per lane before the timed-like replays
+            f, nz = _inputs(8, seeds[0])
+            pl.forward(f, noise=nz)
+        pl.synchronize()
+        outs, junk = [], []
+        for sd_ in seeds:
+            f, nz = _inputs(8, sd_)
+            outs.append(pl.forward(f, noise=nz)["trajectory"])
+            shapes = [(v.shape, v.dtype) for v in f.values()] + [(nz.shape, nz.dtype)]
+            del f, nz
+            # same sizes on the default stream: the caching allocator's first candidates are the dropped blocks
+            junk.append([torch.full(sh, float("nan"), dtype=dt, device=DEV) for sh, dt in shapes])
+        pl.synchronize()
+        for i, o in enumerate(outs):
+            assert torch.equal(o.cpu(), ref[i]), f"batch {i}"
+    finally:
+        pl.close()
+        solo.close()
+
+
+def test_handle_churn_then_two_stream_replay(seeded_sd):
+    """Regression for the round-3 host segfault inside hipGraphLaunch after many handles were created and destroyed
+    (DESIGN.md section 4, Handle lifetime): 32 clones are created, run in both stream modes (eager, captured, replayed;
+    single-stream ones on caller streams) and destroyed, then the first handle's two-stream graph is replayed and
+    must give its earlier result bit for bit."""
+    base = DiffusionDriveModel(state_dict=seeded_sd, device=0)
+    try:
+        f, nz = _inputs(1, 41)
+        ref = [base.forward(f, noise=nz)["trajectory"].cpu() for _ in range(3)][-1]
+        streams = [torch.cuda.Stream(DEV) for _ in range(3)]
+        for i in range(32):
+            c = base.clone()
+            try:
+                single = i % 2 == 1
+                c.set_streams(1 if single else 2)
+                s = streams[i % 3] if single else None
+                for _ in range(3):
+                    if s is not None:
+                        s.wait_stream(torch.cuda.current_stream())
+                        with torch.cuda.stream(s):
+                            out = c.forward(f, noise=nz, stream=s)["trajectory"]
+                        s.synchronize()
+                    else:
+                        out = c.forward(f, noise=nz)["trajectory"]
+                assert float((out.cpu() - ref).abs().max()) <= 1e-5, i
+            finally:
+                c.close()
+        for _ in range(3):
+            again = base.forward(f, noise=nz)["trajectory"].cpu()
+        assert torch.equal(again, ref)
+    finally:
+        base.close()

@@ -110,9 +110,80 @@ def test_runner_lanes_match_one_lane(gpu, seeded_sd):
     runner = BatchedTrajectoryRunner(agent, batch_size=2, lanes=3)
     three = runner.run(toks, inputs.__getitem__)
     assert list(three) == toks and len(runner._clones) == 2
+    assert agent._transfuser_model.stream_count() == 2  # restored to what the runner found
     for t in toks:
         assert np.abs(three[t].poses - one[t].poses).max() <= 1e-5, t
+    runner.close()
+    assert runner._clones == []
+    # a handle the caller configured single-stream stays single-stream
+    agent._transfuser_model.set_streams(1)
+    torch.manual_seed(33)
+    BatchedTrajectoryRunner(agent, batch_size=2, lanes=2).run(toks[:3], inputs.__getitem__)
+    assert agent._transfuser_model.stream_count() == 1
+    agent._transfuser_model.set_streams(2)
     torch.manual_seed(33)
     again = BatchedTrajectoryRunner(agent, batch_size=2).run(toks, inputs.__getitem__)
     for t in toks:
         assert np.array_equal(again[t].poses, one[t].poses), t
+
+
+def test_runner_isolates_failures_per_batch(monkeypatch):
+    """A failure while building one batch's features, launching its forward or finishing it marks THAT batch's
+    tokens failed and the other batches complete (the reference isolates per token: run_pdm_score.py:77-100).
+    CPU: stand-in agent / model / feature builder (the isolation logic only; the GPU path is covered above)."""
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.runner import BatchedTrajectoryRunner
+
+    class _Stream:
+        def synchronize(self):
+            pass
+
+    class _Poison:  # a forward output that fails when the batch is finished
+        def cpu(self):
+            raise RuntimeError("device lost while reading back")
+
+    class _Model:
+        device = 0
+
+        def __init__(self):
+            self.streams = 2
+
+        def stream_count(self):
+            return self.streams
+
+        def set_streams(self, n):
+            self.streams = n
+
+        def numerics_flags(self, clear=True):
+            return 0
+
+        def forward(self, feats, noise=None, safe=False, stream=None):
+            tags = feats["tags"]
+            if "boom" in tags:
+                raise RuntimeError("forward launch failed")
+            if "poison" in tags:
+                return {"trajectory": _Poison()}
+            return {"trajectory": torch.stack([torch.full((8, 3), float(t[1:])) for t in tags])}
+
+    class _Builder:
+        def compute_features_batch(self, inputs):
+            if "badfeat" in inputs:
+                raise ValueError("corrupt sensor blob")
+            return {"tags": list(inputs)}
+
+    class _Agent:
+        _config = TransfuserConfig()
+        _transfuser_model = _Model()
+
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a, **k: _Stream())
+    runner = BatchedTrajectoryRunner.__new__(BatchedTrajectoryRunner)
+    runner.agent, runner.batch_size, runner.lanes, runner._clones = _Agent(), 2, 1, []
+    runner.device, runner.builder, runner.failed = 0, _Builder(), []
+    inputs = {"t0": "t0", "t1": "t1", "t2": "badfeat", "t3": "t3", "t4": "boom", "t5": "t5",
+              "t6": "poison", "t7": "t7", "t8": "t8", "t9": "t9"}
+    got = runner.run(list(inputs), inputs.__getitem__)
+    failed = sorted(t for t, _ in runner.failed)
+    assert failed == ["t2", "t3", "t4", "t5", "t6", "t7"], runner.failed
+    assert sorted(got) == ["t0", "t1", "t8", "t9"]
+    assert float(got["t9"].poses[0, 0]) == 9.0
+    assert _Agent._transfuser_model.streams == 2  # untouched with one lane
