@@ -16,5 +16,5 @@ run() {  # run <name> <timeout> <cmd...>
 }
 run churn_pool1 150 tools/repro/graph_churn 200 1 64 || exit $?
 run churn_pool0 150 tools/repro/graph_churn 200 0 64 || exit $?
-DDMI_STREAM_POOL=0 run order_pool0 600 python -u -m pytest tests/test_runner.py tests/test_inflight_gpu.py tests/test_agent.py \
+run order_pool0 600 env DDMI_STREAM_POOL=0 python -u -m pytest tests/test_runner.py tests/test_inflight_gpu.py tests/test_agent.py \
   -v -m gpu -x --timeout 300 --timeout-method thread || exit $?
