@@ -127,7 +127,10 @@ int dd_get_streams(dd_handle* h, int* n);
  *                  backbone (trunks + GPT fusion), f16x3 after it (FPN, BEV tokens, decoders, heads):
  *                  the REDUCED-precision mode of the bf16 configs (BASELINE configs C2-bf16 / C4),
  *                  held to no worse than the reference's own bf16 autocast (0.06-0.08 m).
- * Default DD_GEMM_FP32, or $DDMI_GEMM=fp32|f16x3|bf16 at dd_create. Attention score GEMMs stay fp32. */
+ * Default DD_GEMM_FP32, or $DDMI_GEMM=fp32|f16x3|bf16 at dd_create. Attention scores: fp32 MFMA in DD_GEMM_FP32;
+ * in DD_GEMM_F16X3 the GPT attention takes f16x3's three products and the tf-decoder megakernel a three-way fp16
+ * split with six products (down to 2^-22); DD_GEMM_BF16 keeps the six-product scores in the GPT attention too
+ * (DESIGN.md section 5). */
 #define DD_GEMM_FP32 0
 #define DD_GEMM_F16X3 1
 #define DD_GEMM_BF16 2

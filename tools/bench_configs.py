@@ -57,6 +57,27 @@ def deviation(o, ref):
                                                ref["poses_reg"].reshape(B * Q, -1, 3))}
 
 
+def bf16_vs_reference(cfg, sd, inp, out, B):
+    """A bf16 row's accuracy against the fp32 CPU oracle on the same batch, beside the reference path's OWN bf16
+    (the oracle under torch.autocast(cpu, bfloat16)): selected-trajectory waypoint L2 (max over scenes) and mode
+    agreement (argmax of the 20 cls logits equal). No bf16 scenes/s is quoted without these (bf16 is reduced
+    precision: near-tied cls logits flip the selected mode)."""
+    from oracle.model import OracleModel
+    om = OracleModel(sd, cfg)
+    args = (inp["camera_feature"], inp["lidar_feature"], inp["status_feature"], inp["noise"])
+    ref = {k: v.numpy() for k, v in om.forward(*args, heads=False).items()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        ac = {k: v.float().numpy() for k, v in om.forward(*args, heads=False).items()}
+
+    def stats(o):
+        return l2(o["trajectory"], ref["trajectory"]), float((o["poses_cls"].argmax(-1) == ref["poses_cls"].argmax(-1)).mean())
+
+    sel, agree = stats(out)
+    asel, aagree = stats(ac)
+    return {"sel_l2_vs_oracle": sel, "agree_vs_oracle": agree, "autocast_sel_l2_vs_oracle": asel,
+            "autocast_agree_vs_oracle": aagree, "oracle_batch": B}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "configs"))
@@ -69,10 +90,14 @@ def main():
     res = {"device": torch.cuda.get_device_name(0), "reps": a.steps, "configs": {}}
     dev = torch.device("cuda:0")
 
+    ctx = {}
+
     def setup(arch, B, seed=1234):
         cfg = TransfuserConfig(image_architecture=arch)
-        m = DiffusionDriveModel(cfg, seeded_state_dict(cfg, 0), device=0)
+        sd = seeded_state_dict(cfg, 0)
+        m = DiffusionDriveModel(cfg, sd, device=0)
         inp = synthetic_inputs(B, seed, cfg)
+        ctx.update(cfg=cfg, sd=sd, inp=inp)
         feats = {k: torch.from_numpy(inp[k]).to(dev) for k in ("camera_feature", "lidar_feature", "status_feature")}
         return m, feats, torch.from_numpy(inp["noise"]).to(dev)
 
@@ -87,6 +112,7 @@ def main():
                           "numerics_flags": m.numerics_flags()}
         rows["bf16"].update(deviation(outs["bf16"], outs["f16x3"]))
         rows["fp32"].update(deviation(outs["fp32"], outs["f16x3"]))
+        rows["bf16"].update(bf16_vs_reference(ctx["cfg"], ctx["sd"], ctx["inp"], outs["bf16"], B))
         res["configs"][key] = {"arch": "resnet34", "batch": B, "ddim_steps": 2, "modes": rows}
         print(key, json.dumps(rows), flush=True)
         m.close()
@@ -101,6 +127,7 @@ def main():
                       "numerics_flags": m.numerics_flags()}
     rows["bf16"].update(deviation(outs["bf16"], outs["f16x3"]))
     rows["fp32"].update(deviation(outs["fp32"], outs["f16x3"]))
+    rows["bf16"].update(bf16_vs_reference(ctx["cfg"], ctx["sd"], ctx["inp"], outs["bf16"], 64))
     res["configs"]["C4_resnet50_batch64"] = {"arch": "resnet50", "batch": 64, "ddim_steps": 2, "modes": rows,
                                              "gflop_per_scene_note": "SURVEY §8d probe: 162.2 GFLOP/scene"}
     print("C4", json.dumps(rows), flush=True)
@@ -202,8 +229,9 @@ def main():
         json.dump(res, f, indent=1)
     lines = [f"# Secondary configs ({res['device']}, synthetic seeded inputs/weights, hipGraph replay, "
              f"{a.steps} reps)", "",
-             "| config | gemm | ms / batch | scenes/s | waypoint L2 vs f16x3 | mode agreement | all-mode L2 |",
-             "|---|---|---|---|---|---|---|"]
+             "| config | gemm | ms / batch | scenes/s | waypoint L2 vs f16x3 | mode agreement | all-mode L2 | "
+             "bf16: selected L2 vs fp32 oracle (reference bf16 autocast) | bf16: mode agreement vs oracle (autocast) |",
+             "|---|---|---|---|---|---|---|---|---|"]
     for key, c in res["configs"].items():
         if "modes" not in c:
             continue
@@ -211,7 +239,9 @@ def main():
             g = lambda k: (f"{r[k]:.3g}" if k in r else "-")  # noqa: E731
             lines.append(f"| {key} | {mode} | {r['ms_per_batch']} | {r['scenes_per_s']} | "
                          f"{g('waypoint_l2_vs_f16x3')} | {g('mode_agreement_vs_f16x3')} | "
-                         f"{g('allmodes_waypoint_l2_vs_f16x3')} |")
+                         f"{g('allmodes_waypoint_l2_vs_f16x3')} | "
+                         f"{g('sel_l2_vs_oracle')} ({g('autocast_sel_l2_vs_oracle')}) | "
+                         f"{g('agree_vs_oracle')} ({g('autocast_agree_vs_oracle')}) |")
     lines += ["", "C5 latency (ms per batch of 64, f16x3) by DDIM steps:", "",
               "| schedule | " + " | ".join(f"N={n}" for n in (1, 2, 4, 5, 6, 8, 10, 20)) + " |",
               "|---|" + "---|" * 8]
