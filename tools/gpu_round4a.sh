@@ -6,6 +6,7 @@
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
 bash tools/gpu_all.sh || exit $?
+bash tools/gpu_x6var.sh || exit $?
 cd "$R"
 run() {  # run <name> <timeout> <cmd...>
   local name=$1 to=$2; shift 2
