@@ -61,6 +61,19 @@ class TransfuserConfig:
     tf_dropout: float = 0.0
     num_bounding_boxes: int = 30                    # :80
 
+    # training-loss weights (:82-89) and the agent-loss option (:22-23)
+    trajectory_weight: float = 12.0
+    trajectory_cls_weight: float = 10.0
+    trajectory_reg_weight: float = 8.0
+    diff_loss_weight: float = 20.0
+    agent_class_weight: float = 10.0
+    agent_box_weight: float = 1.0
+    bev_semantic_weight: float = 14.0
+    latent: bool = False
+    latent_rad_thresh: float = 4 * 3.141592653589793 / 9
+    # forward_train's timestep range: torch.randint(0, 50) (transfuser_model_v2.py:533)
+    train_timestep_max: int = 50
+
     num_bev_classes: int = 7                        # :116
     bev_features_channels: int = 64                 # :117
     bev_down_sample_factor: int = 4                 # :118

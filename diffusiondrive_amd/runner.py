@@ -70,11 +70,15 @@ class BatchedTrajectoryRunner:
         return {t: Trajectory(np.ascontiguousarray(poses[i])) for i, t in enumerate(tokens)}
 
     def _planner(self):
+        """(InFlightPlanner over the agent's handle + clones, each handle's stream count as found: the planner
+        switches every lane to single-stream when there are several)."""
         from .model import InFlightPlanner
         model = self.agent._transfuser_model
         while len(self._clones) < self.lanes - 1:
             self._clones.append(model.clone())
-        return InFlightPlanner(models=[model] + self._clones[:self.lanes - 1])
+        models = [model] + self._clones[:self.lanes - 1]
+        saved = [m.stream_count() for m in models] if len(models) > 1 else []
+        return InFlightPlanner(models=models), saved
 
     def close(self):
         """Release the lane clones' handles (the agent's own handle stays with the agent)."""
@@ -97,9 +101,8 @@ class BatchedTrajectoryRunner:
         lane's numerics flag read - the feature kernels raise none) before its lane takes another batch, so every
         flag belongs to one forward. An exception in one batch's features, launch or finish fails that batch's
         tokens only."""
-        pl = self._planner()
         # every lane runs single-stream while several are in flight; each handle's own count is restored after
-        saved = [m.stream_count() for m in pl.lanes] if len(pl) > 1 else []
+        pl, saved = self._planner()
         for m in pl.lanes:
             m.numerics_flags(clear=True)
             if len(pl) > 1:

@@ -113,6 +113,33 @@ def synthetic_inputs(batch: int, seed: int = 1234, cfg: TransfuserConfig = None)
     }
 
 
+def synthetic_targets(batch: int, seed: int = 1234, cfg: TransfuserConfig = None) -> Dict[str, np.ndarray]:
+    """Synthetic training targets in the reference's target schema (TransfuserTargetBuilder,
+    transfuser_features.py:141-387): ``trajectory`` (B, 8, 3) ego poses of a constant-speed / constant-yaw-rate
+    drive (x forward, metres; heading, radians), ``agent_states`` (B, 30, 5) boxes [x, y, heading, length, width]
+    (BoundingBox2DIndex), ``agent_labels`` (B, 30) validity, ``bev_semantic_map`` (B, 128, 256) class ids in
+    [0, 7) (uint8; the loss takes ``.long()``)."""
+    cfg = cfg or TransfuserConfig()
+    r = np.random.Generator(np.random.PCG64([seed, 11]))
+    P, dt = cfg.trajectory_sampling.num_poses, cfg.trajectory_sampling.interval_length
+    v = r.uniform(0.0, 15.0, (batch, 1))
+    w = r.normal(0.0, 0.12, (batch, 1))
+    tt = dt * np.arange(1, P + 1)[None, :]
+    head = w * tt
+    safe_w = np.where(np.abs(w) < 1e-6, 1e-6, w)
+    x = v * np.sin(safe_w * tt) / safe_w
+    y = v * (1.0 - np.cos(safe_w * tt)) / safe_w
+    traj = np.stack([x, y, head], axis=-1) + r.normal(0.0, 0.2, (batch, P, 3)) * np.array([1.0, 1.0, 0.05])
+    n = cfg.num_bounding_boxes
+    boxes = np.stack([r.uniform(-32, 32, (batch, n)), r.uniform(-32, 32, (batch, n)),
+                      r.uniform(-np.pi, np.pi, (batch, n)), r.uniform(2.0, 6.0, (batch, n)),
+                      r.uniform(1.5, 2.5, (batch, n))], axis=-1)
+    labels = r.random((batch, n)) < 0.3
+    bev = r.integers(0, 7, (batch, cfg.lidar_resolution_height // 2, cfg.lidar_resolution_width)).astype(np.uint8)
+    return {"trajectory": traj.astype(np.float32), "agent_states": boxes.astype(np.float32),
+            "agent_labels": labels, "bev_semantic_map": bev}
+
+
 def reference_noise(batch: int, seed: int, cfg: TransfuserConfig = None) -> np.ndarray:
     """The DDIM start noise exactly as the reference draws it on CPU after
     ``torch.manual_seed(seed)``: ``torch.randn(B, 20, 8, 2)`` (transfuser_model_v2.py:593 is

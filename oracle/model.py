@@ -311,6 +311,114 @@ def trajectory_head(ego_q, agents_q, bev, sd, cfg, noise, steps=None, taps=None,
     return best, reg, cls
 
 
+def trajectory_head_train(ego_q, agents_q, bev, sd, cfg, noise, timesteps, taps=None):
+    """TrajectoryHead.forward_train (transfuser_model_v2.py:520-576) with its two random draws passed in
+    (``timesteps`` ~ randint(0, 50) (B,), ``noise`` ~ randn (B, 20, 8, 2), :533-534): per-scene truncated noise
+    on the normalised plan anchors, clamp, denorm, ONE pass of the cascade decoder with the per-scene time
+    embedding (:537-556). Returns (best_reg, [reg per layer], [cls per layer])."""
+    p = "_trajectory_head"
+    B = ego_q.shape[0]
+    sched = DDIM(cfg.num_train_timesteps)
+    anchor = sd[p + ".plan_anchor"].unsqueeze(0).repeat(B, 1, 1, 1)
+    t = torch.as_tensor(timesteps).to(torch.int64)
+    a = sched.ac[t].view(B, 1, 1, 1)
+    noisy = a ** 0.5 * norm_odo(anchor) + (1 - a) ** 0.5 * noise
+    pts = denorm_odo(torch.clamp(noisy.float(), -1, 1))
+    emb = sine_embed(pts, 64).flatten(-2)
+    tf = linear(emb, sd, p + ".plan_anchor_encoder.0")
+    tf = layer_norm(F.relu(tf), sd, p + ".plan_anchor_encoder.2")
+    tf = linear(tf, sd, p + ".plan_anchor_encoder.3")
+    te = timestep_embed(t)
+    te = linear(mish(linear(te, sd, p + ".time_mlp.1")), sd, p + ".time_mlp.3").view(B, 1, -1)
+    values = [F.relu(conv(bev, sd, f"{p}.diff_decoder.layers.{l}.cross_bev_attention.value_proj.0", 1, 1, bias=True))
+              for l in range(cfg.num_diff_layers)]
+    regs, clss = [], []
+    cur = pts
+    for l in range(cfg.num_diff_layers):
+        reg, cls = diff_layer(tf, cur, bev, agents_q, ego_q, te, sd, f"{p}.diff_decoder.layers.{l}", cfg, values[l],
+                              taps, f"train_l{l}")
+        regs.append(reg)
+        clss.append(cls)
+        cur = reg[..., :2]
+    idx = clss[-1].argmax(-1)
+    return regs[-1][torch.arange(B), idx], regs, clss
+
+
+def sigmoid_focal_loss(pred, target, gamma=2.0, alpha=0.25):
+    """py_sigmoid_focal_loss (multimodal_loss.py:71-114), reduction 'mean', no weight."""
+    ps = pred.sigmoid()
+    target = target.type_as(pred)
+    pt = (1 - ps) * target + ps * (1 - target)
+    fw = (alpha * target + (1 - alpha) * (1 - target)) * pt.pow(gamma)
+    return (F.binary_cross_entropy_with_logits(pred, target, reduction="none") * fw).mean()
+
+
+def loss_computer(reg, cls, target_traj, anchor, cfg):
+    """LossComputer.forward (multimodal_loss.py:131-168): the anchor mode nearest the target (mean over poses of
+    the xy distance) is the class target of a focal loss over the 20 logits and selects the regressed
+    trajectory of an L1 loss against the target (all 3 channels)."""
+    B, M, T, D = reg.shape
+    dist = torch.linalg.norm(target_traj.unsqueeze(1)[..., :2] - anchor, dim=-1).mean(-1)
+    mode = dist.argmin(-1)
+    best = reg[torch.arange(B), mode]
+    onehot = torch.zeros(B, M, dtype=cls.dtype)
+    onehot[torch.arange(B), mode] = 1
+    return (cfg.trajectory_cls_weight * sigmoid_focal_loss(cls, onehot)
+            + cfg.trajectory_reg_weight * F.l1_loss(best, target_traj))
+
+
+def agent_loss(targets, pred, cfg):
+    """_agent_loss (transfuser_loss.py:54-113): BCE + L1 costs, Hungarian matching per scene (scipy, on CPU as
+    the reference), then the matched box L1 over the valid targets and the label BCE."""
+    from scipy.optimize import linear_sum_assignment
+    gt_states = torch.as_tensor(targets["agent_states"])
+    gt_valid = torch.as_tensor(targets["agent_labels"]).bool()
+    ps, pl = pred["agent_states"], pred["agent_labels"]
+    if cfg.latent:
+        rad = torch.arctan2(gt_states[..., 1], gt_states[..., 0])
+        gt_valid = gt_valid & (-cfg.latent_rad_thresh <= rad) & (rad <= cfg.latent_rad_thresh)
+    B, N = ps.shape[:2]
+    n_gt = gt_valid.sum()
+    n_gt = n_gt if n_gt > 0 else n_gt + 1
+    gv = gt_valid[:, :, None].float()
+    pe = pl[:, None, :]
+    mx = torch.relu(-pe)
+    ce = ((1 - gv) * pe + mx + torch.log(torch.exp(-mx) + torch.exp(-pe - mx))).permute(0, 2, 1)
+    l1 = (gt_valid[..., None].float() * (gt_states[:, :, None, :2] - ps[:, None, :, :2]).abs().sum(-1)).permute(0, 2, 1)
+    cost = cfg.agent_class_weight * ce + cfg.agent_box_weight * l1
+    src, dst = [], []
+    for b in range(B):
+        i, j = linear_sum_assignment(cost[b].numpy())
+        src.append(torch.as_tensor(i, dtype=torch.int64))
+        dst.append(torch.as_tensor(j, dtype=torch.int64))
+    bidx = torch.cat([torch.full_like(s_, b) for b, s_ in enumerate(src)])
+    sidx = torch.cat(src)
+    gs_ = torch.cat([gt_states[b][j] for b, j in enumerate(dst)])
+    gvl = torch.cat([gt_valid[b][j] for b, j in enumerate(dst)]).float()
+    box = (F.l1_loss(ps[bidx, sidx], gs_, reduction="none").sum(-1) * gvl).view(B, -1).sum() / n_gt
+    cls = F.binary_cross_entropy_with_logits(pl[bidx, sidx], gvl, reduction="none").view(B, -1).mean()
+    return cls, box
+
+
+def transfuser_loss(targets, pred, cfg):
+    """transfuser_loss (transfuser_loss.py:11-51): weighted sum of the trajectory loss (forward_train's, else L1 of
+    the trajectory), the agent class / box losses and the BEV semantic cross entropy."""
+    if "trajectory_loss" in pred:
+        traj = pred["trajectory_loss"]
+    else:
+        traj = F.l1_loss(pred["trajectory"], torch.as_tensor(targets["trajectory"]))
+    ac, ab = agent_loss(targets, pred, cfg)
+    bev = F.cross_entropy(pred["bev_semantic_map"], torch.as_tensor(targets["bev_semantic_map"]).long())
+    diff = pred.get("diffusion_loss", 0)
+    out = {"loss": cfg.trajectory_weight * traj + cfg.diff_loss_weight * diff + cfg.agent_class_weight * ac
+           + cfg.agent_box_weight * ab + cfg.bev_semantic_weight * bev,
+           "trajectory_loss": cfg.trajectory_weight * traj, "diffusion_loss": cfg.diff_loss_weight * diff,
+           "agent_class_loss": cfg.agent_class_weight * ac, "agent_box_loss": cfg.agent_box_weight * ab,
+           "bev_semantic_loss": cfg.bev_semantic_weight * bev}
+    out.update(pred.get("trajectory_loss_dict", {}))
+    return out
+
+
 # --------------------------------------------------------------------------- full model
 class OracleModel:
     """fp32 CPU restatement of V2TransfuserModel.forward in eval mode (transfuser_model_v2.py:98-162)."""
@@ -322,11 +430,40 @@ class OracleModel:
     @torch.no_grad()
     def forward(self, camera, lidar, status, noise, steps=None, taps: Optional[Taps] = None,
                 heads=True, schedule="truncated") -> Dict[str, torch.Tensor]:
+        nz = torch.as_tensor(np.asarray(noise))
+        ego_q, agents_q, cross, p3 = self._features(camera, lidar, status, taps)
+        traj, reg, cls = trajectory_head(ego_q, agents_q, cross, self.sd, self.cfg, nz, steps, taps, schedule)
+        out = {"trajectory": traj, "poses_reg": reg, "poses_cls": cls}
+        if heads:
+            out.update(self._heads(p3, agents_q))
+        return out
+
+    @torch.no_grad()
+    def forward_train(self, camera, lidar, status, noise, timesteps, targets, taps: Optional[Taps] = None,
+                      heads=True) -> Dict[str, torch.Tensor]:
+        """V2TransfuserModel.forward with targets and the trajectory head in training mode (forward_train,
+        transfuser_model_v2.py:520-576), the rest of the network in eval mode (the deterministic loss evaluator):
+        ``trajectory``, ``trajectory_loss`` (sum over layers), ``trajectory_loss_dict``, the per-layer
+        ``poses_reg_list`` / ``poses_cls_list`` and, with ``heads``, the BEV-semantic / agent outputs."""
+        cfg, sd = self.cfg, self.sd
+        nz = torch.as_tensor(np.asarray(noise))
+        ego_q, agents_q, cross, p3 = self._features(camera, lidar, status, taps)
+        best, regs, clss = trajectory_head_train(ego_q, agents_q, cross, sd, cfg, nz, timesteps, taps)
+        tt = torch.as_tensor(np.asarray(targets["trajectory"]))
+        anchor = sd["_trajectory_head.plan_anchor"].unsqueeze(0).repeat(nz.shape[0], 1, 1, 1)
+        d = {f"trajectory_loss_{i}": loss_computer(r, c, tt, anchor, cfg) for i, (r, c) in enumerate(zip(regs, clss))}
+        out = {"trajectory": best, "trajectory_loss": sum(d.values()), "trajectory_loss_dict": d,
+               "poses_reg_list": regs, "poses_cls_list": clss}
+        if heads:
+            out.update(self._heads(p3, agents_q))
+        return out
+
+    def _features(self, camera, lidar, status, taps=None):
+        """Everything of V2TransfuserModel.forward before the trajectory head (transfuser_model_v2.py:104-158)."""
         cfg, sd = self.cfg, self.sd
         cam = torch.as_tensor(np.asarray(camera))
         lid = torch.as_tensor(np.asarray(lidar))
         st = torch.as_tensor(np.asarray(status))
-        nz = torch.as_tensor(np.asarray(noise))
         B = st.shape[0]
         p3, bev = backbone(cam, lid, sd, cfg, taps)
         bev_tok = conv(bev, sd, "_bev_downscale", bias=True).flatten(-2).permute(0, 2, 1)
@@ -350,18 +487,20 @@ class OracleModel:
             taps.put("keyval", keyval)
             taps.put("cross_bev", cross)
             taps.put("query_out", q)
-        ego_q, agents_q = q[:, :1], q[:, 1:]
-        traj, reg, cls = trajectory_head(ego_q, agents_q, cross, sd, cfg, nz, steps, taps, schedule)
-        out = {"trajectory": traj, "poses_reg": reg, "poses_cls": cls}
-        if heads:
-            h = F.relu(conv(p3, sd, "_bev_semantic_head.0", 1, 1, bias=True))
-            h = conv(h, sd, "_bev_semantic_head.2", bias=True)
-            out["bev_semantic_map"] = F.interpolate(
-                h, size=(cfg.lidar_resolution_height // 2, cfg.lidar_resolution_width),
-                mode="bilinear", align_corners=False)
-            a = linear(F.relu(linear(agents_q, sd, "_agent_head._mlp_states.0")), sd, "_agent_head._mlp_states.2")
-            # BoundingBox2DIndex: POINT = 0:2, HEADING = 2 (transfuser_features.py:388-443)
-            a = torch.cat([torch.tanh(a[..., :2]) * 32, torch.tanh(a[..., 2:3]) * np.pi, a[..., 3:]], -1)
-            out["agent_states"] = a
-            out["agent_labels"] = linear(agents_q, sd, "_agent_head._mlp_label.0").squeeze(-1)
+        return q[:, :1], q[:, 1:], cross, p3
+
+    def _heads(self, p3, agents_q):
+        """_bev_semantic_head and AgentHead (transfuser_model_v2.py:144,159,165-205)."""
+        cfg, sd = self.cfg, self.sd
+        out = {}
+        h = F.relu(conv(p3, sd, "_bev_semantic_head.0", 1, 1, bias=True))
+        h = conv(h, sd, "_bev_semantic_head.2", bias=True)
+        out["bev_semantic_map"] = F.interpolate(
+            h, size=(cfg.lidar_resolution_height // 2, cfg.lidar_resolution_width),
+            mode="bilinear", align_corners=False)
+        a = linear(F.relu(linear(agents_q, sd, "_agent_head._mlp_states.0")), sd, "_agent_head._mlp_states.2")
+        # BoundingBox2DIndex: POINT = 0:2, HEADING = 2 (transfuser_features.py:388-443)
+        a = torch.cat([torch.tanh(a[..., :2]) * 32, torch.tanh(a[..., 2:3]) * np.pi, a[..., 3:]], -1)
+        out["agent_states"] = a
+        out["agent_labels"] = linear(agents_q, sd, "_agent_head._mlp_label.0").squeeze(-1)
         return out
