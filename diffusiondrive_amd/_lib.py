@@ -38,6 +38,13 @@ class DDOutputs(ctypes.Structure):
     ]
 
 
+class DDTrainOutputs(ctypes.Structure):
+    _fields_ = [
+        ("trajectory", c_void_p), ("poses_reg", c_void_p * 2), ("poses_cls", c_void_p * 2), ("loss", c_void_p),
+        ("bev_semantic_map", c_void_p), ("agent_states", c_void_p), ("agent_labels", c_void_p),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dd_default_config": (None, [ctypes.POINTER(DDConfig)]),
@@ -59,6 +66,11 @@ _SIGS = {
     "dd_set_graph": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_set_streams": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_get_streams": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "dd_forward_train": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        ctypes.c_int, ctypes.c_float, ctypes.c_float, c_void_p, c_void_p]),
+    "dd_bev_semantic_loss": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            c_void_p, c_void_p, c_void_p]),
+    "dd_bev_semantic_loss_work": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "dd_set_gemm_mode": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_set_schedule": (ctypes.c_int, [c_void_p, ctypes.c_int]),
     "dd_get_gemm_mode": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int)]),

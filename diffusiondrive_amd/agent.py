@@ -9,8 +9,9 @@ stripped), ``get_sensor_config()``, ``get_feature_builders()``, ``forward(featur
 
 When the real ``navsim`` package is importable the class subclasses its ``AbstractAgent`` and
 returns its ``Trajectory`` / ``SensorConfig``; otherwise it uses the local stand-ins below (the GPU
-box has no navsim). Training entry points (losses, optimizers, target builders) are out of scope
-(SURVEY.md §2 rows 9-10, 17).
+box has no navsim). Training: ``forward`` in training mode runs the trajectory head's forward_train and
+``compute_loss`` the reference's transfuser_loss (a loss evaluator over the inference arithmetic: no backward, no
+batch-statistics BatchNorm, no dropout); optimizers and target builders are out of scope.
 """
 from abc import ABC
 from dataclasses import dataclass, field
@@ -131,12 +132,24 @@ class DiffusionDriveAgent(_Base):
 
     def forward(self, features: Dict[str, torch.Tensor], targets: Dict[str, torch.Tensor] = None,
                 noise: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
-        """transfuser_agent.py:120-125 (eval): returns trajectory plus the auxiliary heads, on the
-        CPU as the reference's CPU-feature forward does (navsim's compute_trajectory calls
-        ``.numpy()`` on it, abstract_agent.py:80-86). Numerics-checked: a f16x3 range overflow
-        re-runs the forward in fp32 (model.forward(safe=True))."""
+        """transfuser_agent.py:120-125. Eval mode: the trajectory plus the auxiliary heads, on the CPU as the
+        reference's CPU-feature forward returns them (navsim's compute_trajectory calls ``.numpy()`` on it,
+        abstract_agent.py:80-86); numerics-checked (a f16x3 range overflow re-runs the forward in fp32).
+        Training mode (``agent.train()``) with targets: the trajectory head's forward_train and its losses
+        (transfuser_model_v2.py:502-576) over the network's inference arithmetic - BatchNorm running statistics and
+        no dropout (the loss evaluator, dd_forward_train); outputs stay on the device for ``compute_loss``."""
+        if self.training and targets is not None:
+            return self._transfuser_model.forward_train(features, targets, noise=noise, heads=True)
         out = self._transfuser_model.forward(features, noise=noise, heads=True, safe=True)
         return {k: v.cpu() for k, v in out.items()}
+
+    def compute_loss(self, features: Dict[str, torch.Tensor], targets: Dict[str, torch.Tensor],
+                     predictions: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """transfuser_agent.py:127-134 -> transfuser_loss (transfuser_loss.py:11-51): the weighted training loss and
+        its terms (diffusiondrive_amd/losses.py). ``predictions`` from ``forward`` in training mode (trajectory
+        loss from forward_train) or eval mode (L1 of the trajectory, the reference's fallback)."""
+        from .losses import transfuser_loss
+        return transfuser_loss(targets, predictions, self._config, self._transfuser_model)
 
     def forward_trajectory(self, features, noise=None, steps=None) -> Dict[str, torch.Tensor]:
         """Trajectory-only fast path (no BEV-semantic / agent heads)."""

@@ -22,13 +22,13 @@ ARCH = os.environ.get("DDMI_ARCH", "gfx950")
 VARIANT = os.environ.get("DDMI_BUILD_VARIANT", "")
 LIB = os.path.join(HERE, "libddmi.so") if not VARIANT else os.path.join(HERE, "_variants", f"libddmi_{VARIANT}.so")
 VARIANT_FLAGS = {"": [], "stamps": ["-DDDMI_MK_STAMPS"], "nopv": ["-DDDMI_MK_STAMPS", "-DDDMI_MK_NOPV"], "x5st": ["-DDDMI_X5_STAMPS"], "x6st": ["-DDDMI_X6_STAMPS"], "nobar": ["-DDDMI_X5_NOBAR", "-DDDMI_X5_STAMPS"], "x6nb": ["-DDDMI_X6_NOBAR"], "dbg": ["-g", "-DDDMI_SEGV_TRACE"]}[VARIANT]
-SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "decoder_mk.hip", "tfdec_mk.hip", "bevproj.hip", "value_proj.hip", "attention.hip", "stem_pool.hip", "features.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
+SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "decoder_mk.hip", "tfdec_mk.hip", "bevproj.hip", "value_proj.hip", "attention.hip", "stem_pool.hip", "features.hip", "train_loss.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", CSRC, "-I", INCLUDE] + VARIANT_FLAGS
 # Elementwise / decoder arithmetic must round like PyTorch-CPU's separate mul and add kernels
 # (no a*b+c -> fma contraction): the DDIM / norm_odo / bilinear-weight chains feed the BEV
 # sampling positions, which are sensitive at the 1e-5 m level.
-PER_SOURCE_FLAGS = {"decoder.hip": ["-ffp-contract=off"], "decoder_mk.hip": ["-ffp-contract=off"], "bevproj.hip": ["-ffp-contract=off"], "tfdec_mk.hip": ["-ffp-contract=off"], "elementwise.hip": ["-ffp-contract=off"],
+PER_SOURCE_FLAGS = {"decoder.hip": ["-ffp-contract=off"], "train_loss.hip": ["-ffp-contract=off"], "decoder_mk.hip": ["-ffp-contract=off"], "bevproj.hip": ["-ffp-contract=off"], "tfdec_mk.hip": ["-ffp-contract=off"], "elementwise.hip": ["-ffp-contract=off"],
                     "runtime.cpp": ["-ffp-contract=off"]}
 
 

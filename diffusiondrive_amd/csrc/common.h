@@ -302,10 +302,12 @@ void launch_avgpool(const float* in, int B, int H, int W, int C, int oh, int ow,
 void launch_bilinear(View4 in, int B, int Hi, int Wi, int C, View4 out, int Ho, int Wo, float ratio_h,
                      float ratio_w, int accumulate, hipStream_t st);
 // Row LayerNorm (eps 1e-5): y[r] = LN(x[r] + res[r / res_div]) * g + b, then optional FiLM
-// y = y * (1 + film_scale) + film_shift. C <= 2048. In-place allowed (y == x).
+// y = y * (1 + film_scale) + film_shift - one FiLM vector for every row, or (film_div > 0) the FiLM vectors of row
+// group r / film_div at film_ld floats apart. C <= 2048. In-place allowed (y == x).
 void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldres, int res_div,
                       const float* g, const float* b, const float* film_scale, const float* film_shift,
-                      float* y, int64_t ldy, int rows, int C, hipStream_t st);
+                      float* y, int64_t ldy, int rows, int C, hipStream_t st, int film_div = 0,
+                      int64_t film_ld = 0);
 // Fused GPT self-attention (attention.hip): y[b,t,h*hs..] = softmax(q.k^T / sqrt(hs)) v per
 // (scene, head) from the packed projection qkv [B][T][3C]; y is [B][T][C]. T % 64 == 0, (T/4) % 8 == 0,
 // T <= 512, hs in {16, ..., 512}.
@@ -373,5 +375,29 @@ void launch_select_mode(const float* cls, const float* reg, float* traj, int* id
                         hipStream_t st);
 // Agent head post-processing: states (rows, 5) in place: [0:2] = tanh*32, [2] = tanh*pi.
 void launch_agent_post(float* states, int rows, hipStream_t st);
+
+// ----------------------------------------------------------------------------------------
+// Training-mode trajectory head / loss evaluator (train_loss.hip; transfuser_model_v2.py:520-576,
+// multimodal_loss.py:119-168, transfuser_loss.py:28-29)
+// per scene: sa = sqrt(ac[t]), s1a = sqrt(1 - ac[t]) (t clamped to [0, tmax))
+void launch_train_coeffs(const int* t, const float* ac, float* sa, float* s1a, int B, int tmax, hipStream_t st);
+// img = sa[b] * norm_odo(anchor) + s1a[b] * noise, (B, QP, 2)
+void launch_train_noisy(const float* anchor, const float* noise, const float* sa, const float* s1a, float* img, int B,
+                        int QP, hipStream_t st);
+// SinusoidalPosEmb(dim) of every scene's integer timestep: out[B][dim]
+void launch_timestep_embed_rows(const int* t, float* out, int B, int dim, hipStream_t st);
+// LossComputer partials per scene: part[b] = (focal sum over the Q logits, L1 sum of the nearest-anchor mode)
+void launch_traj_loss_scene(const float* reg, const float* cls, const float* target, const float* anchor, float* part,
+                            int B, int Q, int P, hipStream_t st);
+// out[0] = cls_w * mean focal + reg_w * mean L1 over the B scenes' partials (index order)
+void launch_traj_loss_reduce(const float* part, float* out, int B, int Q, int P, float cls_w, float reg_w,
+                             hipStream_t st);
+// o[2] = o[0] + o[1] (the summed trajectory loss of the two decoder layers, forward_train :563-565)
+void launch_add2(float* o, hipStream_t st);
+// BEV-semantic cross entropy (mean over B x HW pixels) of NCHW logits against uint8 class ids; part holds
+// bev_ce_partials(B, HW) floats
+size_t bev_ce_partials(int B, int HW);
+void launch_bev_ce(const float* logits, const uint8_t* target, float* part, float* out, int B, int C, int HW,
+                   hipStream_t st);
 
 }  // namespace ddmi

@@ -148,12 +148,7 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // PREC 0: f16x3 (32-channel chunks; a halo pixel row / B slot holds the hi and lo fp16 images of them);
 // PREC 1: bf16 (64-channel chunks; the same bytes hold channels 0-31 and 32-63 of the chunk in bf16, and
 // each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
-// VAR (issue-order variants, DDMI_X6_VAR, read per dispatch): bit 0 - the second half of an 8-wave workgroup (waves
-// 4-7, each sharing a SIMD with one of waves 0-3) at s_setprio 1 for the whole K loop (MI355X_MICROARCH.md "Two waves
-// per SIMD" item 4); bit 1 - every wave opens a step with its MFMAs and issues the step's DMAs and fragment reads
-// after them. (Only one half MFMA-first - item 9's stagger - needs the K loop twice in the kernel: the BN = 128 forms
-// then spill 80 VGPRs.)
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC, int VAR>
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
 __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks, int diag) {
   constexpr int NW = WM * WN, NT = 64 * NW;
@@ -383,27 +378,17 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   // before), every wave's have (barrier), and every wave finished reading step (c, t) - 1.
   // Then: issue B(s + D); at t == TA the halo of chunk c + 1.
   int slot = 0;  // ring slot of the current step
-  auto open_barrier = [&](auto TAP, auto FIRST) {
+  auto open_step = [&](int c, auto TAP, auto FIRST) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
     constexpr int N = (D - 1) * BPS + (halo_in_window(t, D, TA, first) ? ALD : 0);
     step_barrier<N>();
-  };
-  auto open_issue = [&](int c, auto TAP) {
-    constexpr int t = decltype(TAP)::value;
     constexpr int tn = (t + D) % 9;
     int ns = slot + D;
     if (ns >= NSLOT) ns -= NSLOT;
     b_issue(ns, tn, t + D >= 9 ? c + 1 : c);
     if constexpr (t == TA) halo_issue(c + 1);
   };
-  auto open_step = [&](int c, auto TAP, auto FIRST) {
-    open_barrier(TAP, FIRST);
-    open_issue(c, TAP);
-  };
-  if constexpr ((VAR & 1) && NW == 8) {
-    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  }
 
   // ---- prologue: halo of chunk 0, B of steps 0 .. D-1, open step 0, its first fragments
   halo_issue(0);
@@ -418,10 +403,9 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   // step (c, t), software pipelined: [F1 reads] [MFMAs F0] [(t == 8) halo c+1 -> other buffer]
   // [open step s+1] [F0 reads of s+1] [MFMAs F1]: every fragment read is in flight under the
   // previous half-step's MFMAs, and the MFMAs after the barrier need no LDS wait.
-  auto step = [&](int c, auto TAP, auto FIRST, auto MF) {
+  auto step = [&](int c, auto TAP, auto FIRST) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
-    constexpr bool mf = decltype(MF)::value;
     load_frag(F1, slot, c, TAP, std::integral_constant<int, 1>());
     __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs they overlap
     mfma_frag(F0);
@@ -440,37 +424,26 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     constexpr int t1 = (t + 1) % 9;
     const int c1 = t == 8 ? c + 1 : c;
     if (++slot == NSLOT) slot = 0;
-    if constexpr (mf) {
-      open_barrier(std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>());
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_frag(F1);
-      __builtin_amdgcn_sched_barrier(0);
-      open_issue(c1, std::integral_constant<int, t1>());
-      load_frag(F0, slot, c1, std::integral_constant<int, t1>(), std::integral_constant<int, 0>());
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      open_step(c1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>());
-      load_frag(F0, slot, c1, std::integral_constant<int, t1>(), std::integral_constant<int, 0>());
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_frag(F1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    open_step(c1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>());
+    load_frag(F0, slot, c1, std::integral_constant<int, t1>(), std::integral_constant<int, 0>());
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_frag(F1);
+    __builtin_amdgcn_sched_barrier(0);
   };
-  auto chunk = [&](int c, auto FIRST, auto MF) {
-    step(c, std::integral_constant<int, 0>(), FIRST, MF);
-    step(c, std::integral_constant<int, 1>(), FIRST, MF);
-    step(c, std::integral_constant<int, 2>(), FIRST, MF);
-    step(c, std::integral_constant<int, 3>(), FIRST, MF);
-    step(c, std::integral_constant<int, 4>(), FIRST, MF);
-    step(c, std::integral_constant<int, 5>(), FIRST, MF);
-    step(c, std::integral_constant<int, 6>(), FIRST, MF);
-    step(c, std::integral_constant<int, 7>(), FIRST, MF);
-    step(c, std::integral_constant<int, 8>(), FIRST, MF);
+  auto chunk = [&](int c, auto FIRST) {
+    step(c, std::integral_constant<int, 0>(), FIRST);
+    step(c, std::integral_constant<int, 1>(), FIRST);
+    step(c, std::integral_constant<int, 2>(), FIRST);
+    step(c, std::integral_constant<int, 3>(), FIRST);
+    step(c, std::integral_constant<int, 4>(), FIRST);
+    step(c, std::integral_constant<int, 5>(), FIRST);
+    step(c, std::integral_constant<int, 6>(), FIRST);
+    step(c, std::integral_constant<int, 7>(), FIRST);
+    step(c, std::integral_constant<int, 8>(), FIRST);
   };
   X6_STAMP(1);
-  constexpr std::integral_constant<bool, (VAR & 2) != 0> MFIRST;
-  chunk(0, std::true_type(), MFIRST);
-  for (int c = 1; c < nchunks; ++c) chunk(c, std::false_type(), MFIRST);
+  chunk(0, std::true_type());
+  for (int c = 1; c < nchunks; ++c) chunk(c, std::false_type());
   // drain the trailing (all-OOB) DMAs and LDS reads; every wave done with the ring and the halo
   step_barrier<0>();
   X6_STAMP(2);
@@ -573,7 +546,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
 #endif
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC, int VAR>
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
 static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
   ConvArgs a = a_in;
   // fused token pooling: whole tiles only, windows inside tiles, 16-B aligned channel quads
@@ -595,35 +568,21 @@ static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
   // read, bit 1 = skip the output store (WRONG results; tools/gpu_x6exp.sh)
   const char* de = getenv("DDMI_X6_DIAG");
   const int diag = de ? atoi(de) : 0;
-  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, VAR>), dim3(n_sp * ntn), dim3(64 * WM * WN),
-                     0, st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
+  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0,
+                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
   DD_HIP_CHECK(hipGetLastError());
-}
-// issue-order variant (kernel header VAR): the default below, or DDMI_X6_VAR (read per dispatch; micro-benchmarks)
-static int x6_var() {
-  const char* e = getenv("DDMI_X6_VAR");
-  return e ? atoi(e) & 3 : 0;
-}
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
-static void launch_x6_var(const ConvArgs& a, hipStream_t st) {
-  switch (x6_var()) {
-    case 1: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 1>(a, st); break;
-    case 2: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 2>(a, st); break;
-    case 3: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 3>(a, st); break;
-    default: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 0>(a, st); break;
-  }
 }
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
 static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
   if constexpr (SH == 0) {
     if (a.prec == 1) {
-      launch_x6_var<TH, TW, BN, WM, WN, D, NSLOT, SH, 1>(a, st);
+      launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 1>(a, st);
       return;
     }
   } else {
     if (a.prec == 1) throw std::runtime_error("conv_x6: bf16 takes the 8-wave configurations");
   }
-  launch_x6_var<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
+  launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
 }
 
 // Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 / bf16 conv this kernel covers (the

@@ -53,7 +53,8 @@ struct MkArgs {
   const int* slots = nullptr;     // [B][Q*P*4] compact row of each tap, -1 = zero padding
   const float* akv = nullptr;     // [B][30][512] agent K | V
   const float* ego = nullptr;     // [B][256] hoisted ego attention output
-  const float* film = nullptr;    // [512] FiLM scale | shift of this (step, layer)
+  const float* film = nullptr;    // [512] FiLM scale | shift of this (step, layer), or [B][512] (film_stride 512)
+  int film_stride = 0;            // floats between scenes' FiLM vectors (0: one for the batch)
   float* gs_out = nullptr;        // [B*Q][256] BEV attention aggregate (tap)
   float* reg_out = nullptr;       // [B*Q][P][3]
   float* cls_out = nullptr;       // [B*Q]
@@ -77,6 +78,8 @@ struct MkInitArgs {
   int* slots = nullptr;
   int* counts = nullptr;  // [B] distinct tap pixels per scene, or nullptr
   float sa = 0, s1a = 0;
+  const float* sa_b = nullptr;   // per-scene add_noise coefficients (training head, forward_train), or nullptr
+  const float* s1a_b = nullptr;
   int B = 0;
 };
 

@@ -481,8 +481,9 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   __syncthreads();
   stamp(24);
   {
-    const float4 fs = reinterpret_cast<const float4*>(a.film)[lane];
-    const float4 fb = reinterpret_cast<const float4*>(a.film + kD)[lane];
+    const float* film = a.film + (int64_t)b * a.film_stride;  // film_stride 0: one FiLM for the batch
+    const float4 fs = reinterpret_cast<const float4*>(film)[lane];
+    const float4 fb = reinterpret_cast<const float4*>(film + kD)[lane];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int q = wave + 8 * k;
@@ -638,11 +639,12 @@ __global__ __launch_bounds__(256) void decoder_mk_init_kernel(MkInitArgs a) {
   __shared__ float pts[2 * kQP];
   __shared__ int table[4096 + 256];
   const int b = blockIdx.x, tid = threadIdx.x;
+  const float sa = a.sa_b ? a.sa_b[b] : a.sa, s1a = a.s1a_b ? a.s1a_b[b] : a.s1a;  // per scene: training head
   for (int t = tid; t < kQP; t += 256) {
     const int64_t i = (int64_t)b * kQP + t;
     const float ax = a.anchor[t * 2], ay = a.anchor[t * 2 + 1];
-    const float ix = a.sa * norm_x(ax) + a.s1a * a.noise[i * 2];
-    const float iy = a.sa * norm_y(ay) + a.s1a * a.noise[i * 2 + 1];
+    const float ix = sa * norm_x(ax) + s1a * a.noise[i * 2];
+    const float iy = sa * norm_y(ay) + s1a * a.noise[i * 2 + 1];
     a.imgx[i * 2] = ix;
     a.imgx[i * 2 + 1] = iy;
     pts[2 * t] = denorm_x(fminf(fmaxf(ix, -1.f), 1.f));

@@ -283,10 +283,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
                                                         const float* __restrict__ res, int64_t ldres, int res_div,
                                                         const float* __restrict__ g, const float* __restrict__ b,
                                                         const float* __restrict__ fs, const float* __restrict__ fb,
+                                                        int film_div, int64_t film_ld,
                                                         float* y, int64_t ldy, int rows, int C) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
+  if (fs && film_div > 0) {  // per-group FiLM rows (training head: one time embedding per scene)
+    fs += (int64_t)(row / film_div) * film_ld;
+    fb += (int64_t)(row / film_div) * film_ld;
+  }
   float v[32];
   const float* xr = x + (int64_t)row * ldx;
   const float* rr = res ? res + (int64_t)(row / res_div) * ldres : nullptr;
@@ -331,12 +336,17 @@ __global__ __launch_bounds__(256) void layernorm_v4_kernel(const float* __restri
                                                            const float* __restrict__ res, int64_t ldres, int res_div,
                                                            const float* __restrict__ g, const float* __restrict__ b,
                                                            const float* __restrict__ fs, const float* __restrict__ fb,
+                                                           int film_div, int64_t film_ld,
                                                            float* y, int64_t ldy, int rows) {
   constexpr int C = LPR * 4 * VPL;
   const int sub = threadIdx.x % LPR;
   const int row = (blockIdx.x * 256 + threadIdx.x) / LPR;
   const bool live = row < rows;
   const int r = live ? row : rows - 1;  // dead lanes still join the xor reductions
+  if (fs && film_div > 0) {  // per-group FiLM rows (training head: one time embedding per scene)
+    fs += (int64_t)(r / film_div) * film_ld;
+    fb += (int64_t)(r / film_div) * film_ld;
+  }
   const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)r * ldx);
   const float4* rr = res ? reinterpret_cast<const float4*>(res + (int64_t)(r / res_div) * ldres) : nullptr;
   float4 v[VPL];
@@ -395,7 +405,7 @@ __global__ __launch_bounds__(256) void layernorm_v4_kernel(const float* __restri
 
 void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldres, int res_div, const float* g,
                       const float* b, const float* film_scale, const float* film_shift, float* y, int64_t ldy,
-                      int rows, int C, hipStream_t st) {
+                      int rows, int C, hipStream_t st, int film_div, int64_t film_ld) {
   if (C > 2048) throw std::runtime_error("layernorm: C > 2048");
   if (rows == 0) return;
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -407,7 +417,7 @@ void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldr
     const int rd = res_div < 1 ? 1 : res_div;
 #define LNV(L, V)                                                                                                  \
   hipLaunchKernelGGL((layernorm_v4_kernel<L, V>), grid, dim3(256), 0, st, x, ldx, res, ldres, rd, g, b, film_scale, \
-                     film_shift, y, ldy, rows)
+                     film_shift, film_div, film_ld, y, ldy, rows)
     switch (C) {
       case 64: LNV(16, 1); break;
       case 128: LNV(32, 1); break;
@@ -421,7 +431,7 @@ void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldr
     return;
   }
   hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, ldx, res, ldres,
-                     res_div < 1 ? 1 : res_div, g, b, film_scale, film_shift, y, ldy, rows, C);
+                     res_div < 1 ? 1 : res_div, g, b, film_scale, film_shift, film_div, film_ld, y, ldy, rows, C);
   DD_HIP_CHECK(hipGetLastError());
 }
 

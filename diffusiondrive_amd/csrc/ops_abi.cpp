@@ -295,6 +295,17 @@ int dd_op_layernorm(const float* x, const float* res, int res_div, const float* 
   });
 }
 
+int dd_bev_semantic_loss(const float* logits, const unsigned char* target, int B, int C, int H, int W, float* work,
+                         float* loss, void* stream) {
+  return op_guard([&] {
+    if (!logits || !target || !work || !loss || B < 1 || C < 1 || C > 255 || H < 1 || W < 1)
+      throw std::invalid_argument("dd_bev_semantic_loss: null pointer or bad shape");
+    launch_bev_ce(logits, target, work, loss, B, C, H * W, S(stream));
+  });
+}
+
+size_t dd_bev_semantic_loss_work(int B, int H, int W) { return bev_ce_partials(B, H * W); }
+
 int dd_op_softmax_rows(float* x, int rows, int L, float scale, void* stream) {
   return op_guard([&] { launch_softmax_rows(x, L, rows, L, scale, S(stream)); });
 }

@@ -238,6 +238,17 @@ class Model {
   // noise == NULL: the DDIM start noise is drawn on the device (Philox4x32-10 + Box-Muller, keyed by
   // rng_seed; scene s of the stream since dd_set_seed takes draws [s Q P 2, (s + 1) Q P 2))
   uint64_t rng_seed = 0, rng_next = 0;
+  // dd_forward_train (the training-mode trajectory head as a loss evaluator, TrajectoryHead.forward_train
+  // transfuser_model_v2.py:520-576): set for the duration of one such call. The head then runs ONE pass of the two
+  // layers from per-scene noised anchors (timesteps staged in "in_tsteps"), with per-scene time embeddings / FiLM,
+  // and - given targets ("in_target") - LossComputer's per-scene partials per layer (train_loss.hip).
+  bool train = false;
+  const int* train_t = nullptr;        // caller's timesteps of the current chunk (device int32)
+  const float* train_target = nullptr;  // caller's target trajectories of the current chunk (device, or nullptr)
+  float* ac_dev = nullptr;              // alphas_cumprod on the device (per-scene add_noise coefficients)
+  float* train_part = nullptr;          // [2 layers][B][2] LossComputer partials of the whole call
+  size_t train_part_n = 0;
+  float* train_loss_dev = nullptr;      // [3] trajectory_loss_0, _1, sum
 
   Model(const dd_config& c, const void* blob, size_t bytes, int dev) : cfg(c), device(dev) {
     DD_HIP_CHECK(hipSetDevice(device));
@@ -270,6 +281,7 @@ class Model {
     st_main = pooled_stream(device);
     st_side = pooled_stream(device);
     st = st_own = st_main;
+    DD_TRACE("create model %p st_main=%p st_side=%p", (void*)this, (void*)st_main, (void*)st_side);
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
@@ -328,9 +340,14 @@ class Model {
         ac[i] = (float)acc;
       }
     }
+    DD_HIP_CHECK(hipMalloc(&ac_dev, sizeof(ac)));
+    DD_HIP_CHECK(hipMemcpy(ac_dev, ac, sizeof(ac), hipMemcpyHostToDevice));
+    DD_HIP_CHECK(hipMalloc(&train_loss_dev, 4 * sizeof(float)));
   }
 
   ~Model() {
+    DD_TRACE("destroy model %p st_main=%p st_side=%p graphs=%zu", (void*)this, (void*)st_main, (void*)st_side,
+             graphs.size());
     if (ev_out) (void)hipEventSynchronize(ev_out);  // the last forward, also when it ran on a caller's stream
     if (st_main) (void)hipStreamSynchronize(st_main);
     if (st_side) (void)hipStreamSynchronize(st_side);
@@ -343,6 +360,9 @@ class Model {
     if (num_flags) (void)hipFree(num_flags);
     if (in_tab) (void)hipFree(in_tab);
     if (tf_mk_layers) (void)hipFree(tf_mk_layers);
+    if (ac_dev) (void)hipFree(ac_dev);
+    if (train_part) (void)hipFree(train_part);
+    if (train_loss_dev) (void)hipFree(train_loss_dev);
     for (auto& kv : bufs) (void)hipFree(kv.second.first);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& p : pending) {
@@ -705,6 +725,10 @@ class Model {
       ia.counts = counts_of(0, 0);
       ia.sa = vanilla ? 0.0f : std::sqrt(a8);
       ia.s1a = vanilla ? 1.0f : std::sqrt(1.0f - a8);
+      if (train) {  // forward_train: per-scene timesteps (train_time_film)
+        ia.sa_b = bufs.at("train_sa").first;
+        ia.s1a_b = bufs.at("train_s1a").first;
+      }
       ia.B = B;
       launch("decoder", 0, [&] { launch_decoder_mk_init(ia, st); });
       // the packed decoder weights (~8.6 MB) into the MALL before the first layer streams them from HBM
@@ -742,7 +766,12 @@ class Model {
         m.slots = slots_of(si, l);
         m.akv = akv[l];
         m.ego = egos[l];
-        m.film = buf("film_s" + std::to_string(si) + "l" + std::to_string(l), 2 * d);
+        if (train) {
+          m.film = bufs.at("train_film_l" + std::to_string(l)).first;
+          m.film_stride = 2 * d;
+        } else {
+          m.film = buf("film_s" + std::to_string(si) + "l" + std::to_string(l), 2 * d);
+        }
         m.gs_out = buf("gs" + sf, (size_t)R * d);
         m.reg_out = buf("reg" + sf, (size_t)R * P * 3);
         m.cls_out = buf("cls" + sf, R);
@@ -780,6 +809,7 @@ class Model {
     join();  // the heads branch on the side stream
     alias("poses_reg", reg_last);
     alias("poses_cls", cls_last);
+    train_loss_partials(B);
   }
 
   // ------------------------------------------------------------------ runtime helpers
@@ -1091,9 +1121,10 @@ class Model {
   }
 
   void ln(const LNp& p, const float* x, int64_t ldx, float* y, int64_t ldy, int rows, const float* res = nullptr,
-          int64_t ldres = 0, int res_div = 1, const float* fs = nullptr, const float* fb = nullptr) {
+          int64_t ldres = 0, int res_div = 1, const float* fs = nullptr, const float* fb = nullptr, int film_div = 0,
+          int64_t film_ld = 0) {
     launch("layernorm", 0, [&] {
-      launch_layernorm(x, ldx, res, ldres, res_div, W(p.g), W(p.b), fs, fb, y, ldy, rows, p.c, st);
+      launch_layernorm(x, ldx, res, ldres, res_div, W(p.g), W(p.b), fs, fb, y, ldy, rows, p.c, st, film_div, film_ld);
     });
   }
 
@@ -1254,6 +1285,10 @@ class Model {
     float* sem = nullptr;
     float* ag_states = nullptr;
     float* ag_labels = nullptr;
+    // forward_train: every layer's poses_reg / poses_cls and LossComputer partials ([B][2] per layer)
+    float* reg_l[2] = {nullptr, nullptr};
+    float* cls_l[2] = {nullptr, nullptr};
+    float* part_l[2] = {nullptr, nullptr};
   };
 
   // denoise timesteps. truncated: roll_timesteps = round(arange(steps) * step_span / steps)[::-1]
@@ -1301,6 +1336,40 @@ class Model {
     }
   }
 
+  // training head: time_mlp(SinusoidalPosEmb(t_b)) -> Mish -> FiLM scale / shift of both layers for every scene
+  // (forward_train :549-551, ModulationLayer :259-294), and the per-scene add_noise coefficients
+  void train_time_film(int B) {
+    const int d = 256;
+    const int* t = reinterpret_cast<const int*>(bufs.at("in_tsteps").first);
+    float* te0 = buf("train_temb0", (size_t)B * d);
+    float* te1 = buf("train_temb1", (size_t)B * 4 * d);
+    float* te2 = buf("train_temb2", (size_t)B * d);
+    float* mte = buf("train_temb_mish", (size_t)B * d);
+    launch("misc", 0, [&] { launch_timestep_embed_rows(t, te0, B, d, st); });
+    gemm(tm1, te0, d, B, te1, 4 * d);
+    launch("misc", 0, [&] { launch_activation(te1, te1, (int64_t)B * 4 * d, 0, st); });
+    gemm(tm3, te1, 4 * d, B, te2, d);
+    launch("misc", 0, [&] { launch_activation(te2, mte, (int64_t)B * d, 0, st); });
+    for (int l = 0; l < 2; ++l) gemm(dl[l].film, mte, d, B, buf("train_film_l" + std::to_string(l), (size_t)B * 2 * d), 2 * d);
+    float* sa = buf("train_sa", B);
+    float* s1a = buf("train_s1a", B);
+    launch("misc", 0, [&] { launch_train_coeffs(t, ac_dev, sa, s1a, B, 1000, st); });
+  }
+
+  // training head with targets: LossComputer's per-scene partials of both layers into "train_part_l*"
+  void train_loss_partials(int B) {
+    if (!train || !train_target) return;
+    const int Q = cfg.num_modes, P = cfg.num_poses;
+    for (int l = 0; l < 2; ++l) {
+      const std::string sf = "_s0l" + std::to_string(l);
+      float* part = buf("train_part_l" + std::to_string(l), (size_t)2 * B);
+      launch("misc", 0, [&] {
+        launch_traj_loss_scene(bufs.at("reg" + sf).first, bufs.at("cls" + sf).first, bufs.at("in_target").first,
+                               W(anchor), part, B, Q, P, st);
+      });
+    }
+  }
+
   void forward_body(int B, int steps, bool heads) {
     const int d = 256, Q = cfg.num_modes, P = cfg.num_poses;
     const int HC = cfg.cam_h, WC = cfg.cam_w, HL = cfg.lidar_h, WL = cfg.lidar_w;
@@ -1342,6 +1411,7 @@ class Model {
     alias("bev_feature", xl);  // (B, 8, 8, 512) NHWC; transformer_decoder_join -> fused = lidar (:204-205)
     // everything past the backbone runs in the head arithmetic (bf16 mode: f16x3; see head_mode)
     ModeScope head_scope(this, head_mode());
+    if (train) train_time_film(B);
 
     // ---- BEV tokens + status -> keyval (B, 65, 256) (+= _keyval_embedding)
     float* KV = buf("keyval", (size_t)B * 65 * d);
@@ -1554,7 +1624,13 @@ class Model {
       // vanilla (C5 ablation): x_T = noise (sa = 0, s1a = 1 keep it bit-exact)
       const float a8 = ac[cfg.trunc_timestep];
       const float sa = vanilla ? 0.0f : std::sqrt(a8), s1a = vanilla ? 1.0f : std::sqrt(1.0f - a8);
-      launch("misc", 0, [&] { launch_ddim_init(W(anchor), noise, imgx, B, Q * P, sa, s1a, st); });
+      if (train)  // forward_train: per-scene timesteps (train_time_film)
+        launch("misc", 0, [&] {
+          launch_train_noisy(W(anchor), noise, bufs.at("train_sa").first, bufs.at("train_s1a").first, imgx, B, Q * P,
+                             st);
+        });
+      else
+        launch("misc", 0, [&] { launch_ddim_init(W(anchor), noise, imgx, B, Q * P, sa, s1a, st); });
     }
     float* pts = buf("pts", (size_t)R * P * 2);
     float* pts2 = buf("pts_next", (size_t)R * P * 2);
@@ -1672,7 +1748,12 @@ class Model {
         // ffn -> norm3 -> FiLM time modulation
         gemm(w.ffn0, x3, d, R, hf, 1024, true);
         gemm(w.ffn2, hf, 1024, R, x2, d);
-        ln(w.n3, x2, d, x2, d, R, nullptr, 0, 1, ss, ss + d);
+        if (train) {  // one FiLM vector per scene (its Q rows)
+          const float* fl = bufs.at("train_film_l" + std::to_string(l)).first;
+          ln(w.n3, x2, d, x2, d, R, nullptr, 0, 1, fl, fl + d, Q, 2 * d);
+        } else {
+          ln(w.n3, x2, d, x2, d, R, nullptr, 0, 1, ss, ss + d);
+        }
         // task decoder: cls branch on the side stream beside the reg branch (and the next layer)
         float* cls = buf("cls" + sfx, R);
         fork();
@@ -1705,6 +1786,7 @@ class Model {
     launch("misc", 0, [&] { launch_select_mode(cls_last, reg_last, traj, idx, B, Q, P, st); });
     alias("poses_reg", reg_last);
     alias("poses_cls", cls_last);
+    train_loss_partials(B);
   }
 
   std::map<std::string, float*> aliases;
@@ -1727,6 +1809,14 @@ class Model {
       launch("misc", 0, [&] { launch_nchw_to_nhwc(lidar, lid4, B, cfg.lidar_channels, cfg.lidar_h, cfg.lidar_w, 4, st); });
     }
     DD_HIP_CHECK(hipMemcpyAsync(st_in, status, sizeof(float) * B * 8, hipMemcpyDeviceToDevice, st));
+    if (train) {
+      float* tb = buf("in_tsteps", (size_t)B);
+      DD_HIP_CHECK(hipMemcpyAsync(tb, train_t, sizeof(int) * B, hipMemcpyDeviceToDevice, st));
+      if (train_target) {
+        float* tg = buf("in_target", (size_t)B * cfg.num_poses * 3);
+        DD_HIP_CHECK(hipMemcpyAsync(tg, train_target, sizeof(float) * B * cfg.num_poses * 3, hipMemcpyDeviceToDevice, st));
+      }
+    }
     if (noise)
       DD_HIP_CHECK(hipMemcpyAsync(nz, noise, sizeof(float) * B * per, hipMemcpyDeviceToDevice, st));
     else
@@ -1775,6 +1865,63 @@ class Model {
     if (!noise) rng_next += (uint64_t)B;
   }
 
+  // The training-mode trajectory head (forward_train, transfuser_model_v2.py:520-576) over the eval-mode network, as
+  // a loss evaluator: per-scene timesteps / noise in, every layer's poses out, and with targets the LossComputer losses
+  // (multimodal_loss.py:119-168) of both layers and their sum (loss[3]), reduced over the whole batch after its chunks.
+  void forward_train(const float* camera, const float* lidar, const float* status, const float* noise,
+                     const int* timesteps, const float* target, int B, const Outs& o, float* loss, float cls_w,
+                     float reg_w, hipStream_t caller) {
+    if (B <= 0) throw std::invalid_argument("batch must be positive");
+    if (!camera || !lidar || !status || !noise || !timesteps || !o.traj)
+      throw std::invalid_argument("dd_forward_train: null input / output pointer (noise and timesteps are required)");
+    if (loss && !target) throw std::invalid_argument("dd_forward_train: loss requested without targets");
+    const int Q = cfg.num_modes, P = cfg.num_poses;
+    if (target && train_part_n < (size_t)B) {
+      DD_HIP_CHECK(hipDeviceSynchronize());  // an earlier call's reduction may still read the old buffer
+      if (train_part) DD_HIP_CHECK(hipFree(train_part));
+      train_part = nullptr;
+      DD_HIP_CHECK(hipMalloc(&train_part, sizeof(float) * 4 * (size_t)B));
+      train_part_n = (size_t)B;
+    }
+    struct Reset {
+      Model& m;
+      ~Reset() {
+        m.train = false;
+        m.train_t = nullptr;
+        m.train_target = nullptr;
+      }
+    } reset{*this};
+    train = true;
+    const int nch = (B + max_chunk - 1) / max_chunk, chunk = (B + nch - 1) / nch;
+    for (int b0 = 0; b0 < B; b0 += chunk) {
+      const int n = std::min(chunk, B - b0);
+      auto off = [&](const float* p, size_t per) { return p ? p + (size_t)b0 * per : nullptr; };
+      auto offw = [&](float* p, size_t per) { return p ? p + (size_t)b0 * per : nullptr; };
+      Outs oc;
+      oc.traj = offw(o.traj, (size_t)P * 3);
+      oc.sem = offw(o.sem, (size_t)7 * (cfg.lidar_h / 2) * cfg.lidar_w);
+      oc.ag_states = offw(o.ag_states, (size_t)30 * 5);
+      oc.ag_labels = offw(o.ag_labels, (size_t)30);
+      for (int l = 0; l < 2; ++l) {
+        oc.reg_l[l] = o.reg_l[l] ? o.reg_l[l] + (size_t)b0 * Q * P * 3 : nullptr;
+        oc.cls_l[l] = o.cls_l[l] ? o.cls_l[l] + (size_t)b0 * Q : nullptr;
+        oc.part_l[l] = target ? train_part + (size_t)l * 2 * B + (size_t)b0 * 2 : nullptr;
+      }
+      train_t = timesteps + b0;
+      train_target = target ? target + (size_t)b0 * P * 3 : nullptr;
+      forward_chunk(off(camera, (size_t)3 * cfg.cam_h * cfg.cam_w),
+                    off(lidar, (size_t)cfg.lidar_channels * cfg.lidar_h * cfg.lidar_w), off(status, 8),
+                    off(noise, (size_t)Q * P * 2), n, 1, oc, caller, 0);
+    }
+    if (target) {
+      // the batch means of both layers and their sum, on the caller's stream (every chunk handed back to it)
+      launch_traj_loss_reduce(train_part, train_loss_dev, B, Q, P, cls_w, reg_w, caller);
+      launch_traj_loss_reduce(train_part + 2 * (size_t)B, train_loss_dev + 1, B, Q, P, cls_w, reg_w, caller);
+      launch_add2(train_loss_dev, caller);
+      if (loss) DD_HIP_CHECK(hipMemcpyAsync(loss, train_loss_dev, 3 * sizeof(float), hipMemcpyDeviceToDevice, caller));
+    }
+  }
+
   // Single-stream forwards (dd_set_streams(h, 1)) called on a non-default stream run on the CALLER's stream
   // itself: no hand-off through the handle's own stream, so N handles driven from N caller streams (N batches
   // in flight) occupy N hardware queues, not 2N (the device has 4 per process by default; streams beyond them
@@ -1810,7 +1957,8 @@ class Model {
     DD_TRACE("film");
     if (generation != gen0) known_shapes.clear();
     const std::string key = std::to_string(B) + "/" + std::to_string(steps) + "/" + std::to_string(heads) + "/g" +
-                            std::to_string(gemm_mode) + "/s" + std::to_string(schedule);
+                            std::to_string(gemm_mode) + "/s" + std::to_string(schedule) +
+                            (train ? (train_target ? "/train1" : "/train0") : "");
     if (use_graph && !profiling && known_shapes.count(key)) {
       if (graph_gen != generation || graphs.size() > 8) {
         // an earlier replay may still run (on the caller's stream in direct mode): ev_out marks the last forward
@@ -1836,10 +1984,11 @@ class Model {
         DD_HIP_CHECK(hipStreamEndCapture(st, &g));
         DD_TRACE("end capture");
         DD_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-        DD_TRACE("instantiated");
+        DD_TRACE("instantiated exec %p on st=%p (model %p)", (void*)ex, (void*)st, (void*)this);
         DD_HIP_CHECK(hipGraphDestroy(g));
         it = graphs.emplace(key, ex).first;
       }
+      DD_TRACE("launch exec %p on st=%p (model %p)", (void*)it->second, (void*)st, (void*)this);
       DD_HIP_CHECK(hipGraphLaunch(it->second, st));
       DD_TRACE("launched");
     } else {
@@ -1860,6 +2009,14 @@ class Model {
       copy_out(o.sem, "bev_semantic_map", (size_t)B * 7 * (cfg.lidar_h / 2) * cfg.lidar_w);
       copy_out(o.ag_states, "agent_states", (size_t)B * 30 * 5);
       copy_out(o.ag_labels, "agent_labels", (size_t)B * 30);
+    }
+    if (train) {
+      for (int l = 0; l < 2; ++l) {
+        const std::string sf = "_s0l" + std::to_string(l);
+        copy_out(o.reg_l[l], "reg" + sf, (size_t)B * Q * P * 3);
+        copy_out(o.cls_l[l], "cls" + sf, (size_t)B * Q);
+        if (train_target) copy_out(o.part_l[l], "train_part_l" + std::to_string(l), (size_t)B * 2);
+      }
     }
     // ev_out marks the end of this forward on whichever stream it ran (dd_numerics_flags / dd_tap wait for it)
     DD_HIP_CHECK(hipEventRecord(ev_out, st));
@@ -1967,6 +2124,26 @@ int dd_forward_ex(dd_handle* h, const float* camera, const float* lidar, const f
     o.ag_states = outs->agent_states;
     o.ag_labels = outs->agent_labels;
     h->m->forward(camera, lidar, status, noise, B, steps, o, static_cast<hipStream_t>(stream));
+  });
+}
+
+int dd_forward_train(dd_handle* h, const float* camera, const float* lidar, const float* status, const float* noise,
+                     const int* timesteps, const float* target_traj, int B, float cls_weight, float reg_weight,
+                     const dd_train_outputs* outs, void* stream) {
+  return guarded([&] {
+    if (!h || !outs) throw std::invalid_argument("dd_forward_train: null handle/outputs");
+    std::lock_guard<std::mutex> lk(h->mu);
+    Model::Outs o;
+    o.traj = outs->trajectory;
+    o.sem = outs->bev_semantic_map;
+    o.ag_states = outs->agent_states;
+    o.ag_labels = outs->agent_labels;
+    for (int l = 0; l < 2; ++l) {
+      o.reg_l[l] = outs->poses_reg[l];
+      o.cls_l[l] = outs->poses_cls[l];
+    }
+    h->m->forward_train(camera, lidar, status, noise, timesteps, target_traj, B, o, outs->loss, cls_weight, reg_weight,
+                        static_cast<hipStream_t>(stream));
   });
 }
 

@@ -246,6 +246,77 @@ class DiffusionDriveModel:
 
     __call__ = forward
 
+    def forward_train(self, features: Dict[str, torch.Tensor], targets: Optional[Dict[str, torch.Tensor]] = None,
+                      timesteps: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
+                      heads: bool = True, stream: Optional[torch.cuda.Stream] = None) -> Dict[str, torch.Tensor]:
+        """V2TransfuserModel.forward(features, targets) with the trajectory head in training mode
+        (TrajectoryHead.forward_train, transfuser_model_v2.py:520-576) over the eval-mode network (dropout off,
+        BatchNorm running statistics): the deterministic loss evaluator (dd_forward_train).
+
+        ``timesteps`` (B,) and ``noise`` (B, 20, 8, 2) are forward_train's two random draws; None draws them as the
+        reference does, in its order, from the global CPU generator (``torch.randint(0, 50, (B,))`` then
+        ``torch.randn``, :533-534). Returns ``trajectory`` (the last layer's argmax mode), ``poses_reg_list`` /
+        ``poses_cls_list`` (every layer), ``timesteps`` / ``noise`` (the draws used) and, with ``targets``
+        (``trajectory`` (B, 8, 3)), ``trajectory_loss`` and ``trajectory_loss_dict`` (LossComputer per layer,
+        modules/multimodal_loss.py:119-168) as 0-d tensors; ``heads`` adds the BEV-semantic / agent outputs."""
+        cfg = self.config
+        dev = torch.device(f"cuda:{self.device}")
+        s = stream or torch.cuda.current_stream(dev)
+        B = torch.as_tensor(features["status_feature"]).shape[0]
+        Q, P = cfg.num_modes, cfg.trajectory_sampling.num_poses
+        if timesteps is None:
+            timesteps = torch.randint(0, cfg.train_timestep_max, (B,))
+        if noise is None:
+            noise = torch.randn((B, Q, P, 2))
+        with torch.cuda.stream(s):
+            cam = self._dev(features["camera_feature"])
+            lid = self._dev(features["lidar_feature"])
+            st = self._dev(features["status_feature"])
+            nz = self._dev(noise)
+            tt = self._dev(timesteps, dtype=torch.int32)
+            if tuple(nz.shape) != (B, Q, P, 2) or tuple(tt.shape) != (B,):
+                raise ValueError(f"noise must be (B,{Q},{P},2) and timesteps (B,), got {tuple(nz.shape)}, {tuple(tt.shape)}")
+            if int(tt.min()) < 0 or int(tt.max()) >= cfg.num_train_timesteps:
+                raise ValueError(f"timesteps must lie in [0, {cfg.num_train_timesteps})")
+            tg = None
+            if targets is not None and targets.get("trajectory") is not None:
+                tg = self._dev(targets["trajectory"])
+                if tuple(tg.shape) != (B, P, 3):
+                    raise ValueError(f"targets['trajectory'] must be (B,{P},3), got {tuple(tg.shape)}")
+            for t in (cam, lid, st, nz, tt, tg):
+                if t is not None:
+                    t.record_stream(s)
+            res = {"trajectory": torch.empty((B, P, 3), device=dev),
+                   "poses_reg_list": [torch.empty((B, Q, P, 3), device=dev) for _ in range(2)],
+                   "poses_cls_list": [torch.empty((B, Q), device=dev) for _ in range(2)]}
+            outs = _lib.DDTrainOutputs()
+            outs.trajectory = res["trajectory"].data_ptr()
+            for l in range(2):
+                outs.poses_reg[l] = res["poses_reg_list"][l].data_ptr()
+                outs.poses_cls[l] = res["poses_cls_list"][l].data_ptr()
+            loss = None
+            if tg is not None:
+                loss = torch.empty(3, device=dev)
+                outs.loss = loss.data_ptr()
+            if heads:
+                res["bev_semantic_map"] = torch.empty((B, 7, cfg.lidar_resolution_height // 2,
+                                                       cfg.lidar_resolution_width), device=dev)
+                res["agent_states"] = torch.empty((B, cfg.num_bounding_boxes, 5), device=dev)
+                res["agent_labels"] = torch.empty((B, cfg.num_bounding_boxes), device=dev)
+                outs.bev_semantic_map = res["bev_semantic_map"].data_ptr()
+                outs.agent_states = res["agent_states"].data_ptr()
+                outs.agent_labels = res["agent_labels"].data_ptr()
+            _lib.check(self.lib.dd_forward_train(self.handle, cam.data_ptr(), lid.data_ptr(), st.data_ptr(),
+                                                 nz.data_ptr(), tt.data_ptr(), tg.data_ptr() if tg is not None else None,
+                                                 B, float(cfg.trajectory_cls_weight), float(cfg.trajectory_reg_weight),
+                                                 ctypes.byref(outs), s.cuda_stream), self.lib)
+        res["timesteps"] = torch.as_tensor(timesteps)
+        res["noise"] = torch.as_tensor(noise)
+        if loss is not None:
+            res["trajectory_loss_dict"] = {"trajectory_loss_0": loss[0], "trajectory_loss_1": loss[1]}
+            res["trajectory_loss"] = loss[2]
+        return res
+
     # ------------------------------------------------------------------ instrumentation
     def tap(self, name: str, shape=None) -> torch.Tensor:
         """Copy a named internal buffer of the last forward (NHWC device layout) to a tensor."""

@@ -61,6 +61,17 @@ typedef struct dd_outputs {
   float* agent_labels;     /* B x 30 */
 } dd_outputs;
 
+/* Outputs of dd_forward_train (device pointers; NULL = not requested). */
+typedef struct dd_train_outputs {
+  float* trajectory;       /* B x P x 3: the last layer's argmax mode (required) */
+  float* poses_reg[2];     /* per decoder layer: B x Q x P x 3 */
+  float* poses_cls[2];     /* per decoder layer: B x Q */
+  float* loss;             /* 3 floats: trajectory_loss_0, trajectory_loss_1, trajectory_loss (needs targets) */
+  float* bev_semantic_map; /* B x 7 x (lidar_h/2) x lidar_w, NCHW */
+  float* agent_states;     /* B x 30 x 5 */
+  float* agent_labels;     /* B x 30 */
+} dd_train_outputs;
+
 /* Fill *cfg with the reference defaults. */
 void dd_default_config(dd_config* cfg);
 
@@ -82,6 +93,26 @@ int dd_forward(dd_handle* h, const float* camera, const float* lidar, const floa
 
 int dd_forward_ex(dd_handle* h, const float* camera, const float* lidar, const float* status, const float* noise,
                   int B, int steps, const dd_outputs* outs, void* stream);
+
+/* The training-mode trajectory head over the eval-mode network, as a loss evaluator: replaces
+ * V2TransfuserModel.forward(features, targets) with TrajectoryHead.forward_train (transfuser_model_v2.py:520-576) and
+ * LossComputer (modules/multimodal_loss.py:119-168). forward_train's two random draws are inputs: timesteps (B
+ * int32 in [0, 1000); the reference draws torch.randint(0, 50)) and noise (B,Q,P,2, torch.randn). The head noises the
+ * normalised plan anchors per scene (diffusers add_noise), clamps, runs ONE pass of both decoder layers with each
+ * scene's own time embedding, and returns every layer's poses; with target_traj (B,P,3) it also returns the
+ * layers' losses cls_weight * focal + reg_weight * L1 (the reference's trajectory_cls_weight 10 / reg_weight 8) and
+ * their sum. Every submodule is in eval mode (dropout off, BatchNorm running statistics). Any B >= 1 (chunks of at
+ * most 128; the loss is reduced over the whole batch). */
+int dd_forward_train(dd_handle* h, const float* camera, const float* lidar, const float* status, const float* noise,
+                     const int* timesteps, const float* target_traj, int B, float cls_weight, float reg_weight,
+                     const dd_train_outputs* outs, void* stream);
+/* The BEV-semantic term of the training loss, transfuser_loss.py:28-29 (F.cross_entropy(bev_semantic_map,
+ * target.long()), mean over every pixel): logits (B,C,H,W) NCHW and target (B,H,W) uint8 class ids in device memory,
+ * work = dd_bev_semantic_loss_work(B, H, W) floats of device scratch, loss = one device float. Deterministic (fixed
+ * reduction order). */
+int dd_bev_semantic_loss(const float* logits, const unsigned char* target, int B, int C, int H, int W, float* work,
+                         float* loss, void* stream);
+size_t dd_bev_semantic_loss_work(int B, int H, int W);
 
 int dd_destroy(dd_handle* h);
 
