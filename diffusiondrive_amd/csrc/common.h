@@ -281,6 +281,7 @@ struct VprojArgs {
   unsigned* flags = nullptr;
   int max_splits = 3;  // 1..3 (DDMI_VPROJ_SPLITS: tests / A/B)
   int max_wgs = 256;   // workgroup budget for (tiles x splits): the CUs not held by a concurrent kernel
+  int nsplit = 1;      // 1: 256-channel tiles (K split up to max_splits); 2: two 128-channel halves, no K split
 };
 bool vproj_supported(int C, int Cout, int H, int W);
 size_t vproj_tiles(int B, int cap);

@@ -71,9 +71,13 @@ __device__ inline void dma6(x6i4 rsrc, uint32_t lds_wave, uint32_t voff) {
                : "memory");
 }
 
+template <int NTL>
 __device__ inline x6f4 vload6(x6i4 rsrc, uint32_t voff) {
   x6f4 v;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
+  if constexpr (NTL)  // nontemporal: the streamed activation halo does not displace the weight slices in L2
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
+  else
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
   return v;
 }
 
@@ -148,7 +152,9 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // PREC 0: f16x3 (32-channel chunks; a halo pixel row / B slot holds the hi and lo fp16 images of them);
 // PREC 1: bf16 (64-channel chunks; the same bytes hold channels 0-31 and 32-63 of the chunk in bf16, and
 // each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
+// NTL: cache policy of the activation streams (DDMI_X6_NT, read per dispatch): bit 0 = the halo loads nontemporal,
+// bit 1 = the epilogue's residual loads nontemporal.
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC, int NTL>
 __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks, int diag) {
   constexpr int NW = WM * WN, NT = 64 * NW;
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
 #pragma unroll
     for (int i = 0; i < ALD; ++i) {
       const int ho = HKEEP ? hofs[HKEEP ? i : 0] : hofs_of(i);
-      hr[i] = vload6(rin, (cv && ho >= 0) ? (uint32_t)(ho + co) * 4u : kOOB6);
+      hr[i] = vload6<NTL & 1>(rin, (cv && ho >= 0) ? (uint32_t)(ho + co) * 4u : kOOB6);
     }
   };
   auto halo_tie = [&]() {  // after a wait: no use of the staged registers may move above it
@@ -476,7 +482,11 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
       const int oy = oy0 + p / TW, ox = ox0 + p % TW;
       const bool ok = nv && oy < a.Ho && ox < a.Wo;
       ooff[k] = ok ? oy * osh + ox * osw : -1;
-      rv[k] = (res && ok) ? *reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw)) : (x6f4){0.f, 0.f, 0.f, 0.f};
+      rv[k] = (x6f4){0.f, 0.f, 0.f, 0.f};
+      if (res && ok) {
+        const x6f4* rp = reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw));
+        rv[k] = (NTL & 2) ? __builtin_nontemporal_load(rp) : *rp;
+      }
     }
   };
   if constexpr (EARLY) load_res();
@@ -546,7 +556,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
 #endif
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC, int NTL>
 static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
   ConvArgs a = a_in;
   // fused token pooling: whole tiles only, windows inside tiles, 16-B aligned channel quads
@@ -568,21 +578,34 @@ static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
   // read, bit 1 = skip the output store (WRONG results; tools/gpu_x6exp.sh)
   const char* de = getenv("DDMI_X6_DIAG");
   const int diag = de ? atoi(de) : 0;
-  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0,
-                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
+  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, NTL>), dim3(n_sp * ntn), dim3(64 * WM * WN),
+                     0, st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
   DD_HIP_CHECK(hipGetLastError());
+}
+static int x6_nt() {
+  const char* e = getenv("DDMI_X6_NT");
+  return e ? atoi(e) & 3 : 0;
+}
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
+static void launch_x6_nt(const ConvArgs& a, hipStream_t st) {
+  switch (x6_nt()) {
+    case 1: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 1>(a, st); break;
+    case 2: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 2>(a, st); break;
+    case 3: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 3>(a, st); break;
+    default: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 0>(a, st); break;
+  }
 }
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
 static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
   if constexpr (SH == 0) {
     if (a.prec == 1) {
-      launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 1>(a, st);
+      launch_x6_nt<TH, TW, BN, WM, WN, D, NSLOT, SH, 1>(a, st);
       return;
     }
   } else {
     if (a.prec == 1) throw std::runtime_error("conv_x6: bf16 takes the 8-wave configurations");
   }
-  launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
+  launch_x6_nt<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
 }
 
 // Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 / bf16 conv this kernel covers (the

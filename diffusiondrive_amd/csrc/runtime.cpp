@@ -199,6 +199,7 @@ class Model {
   bool value_splitk = true;          // DDMI_VALUE_SPLITK=0: the gathered value_proj on conv_x3 (one launch, K whole)
   int vproj_splits = 3;              // DDMI_VPROJ_SPLITS: most K splits of value_proj.hip (1..3)
   bool vproj_splits_env = false;     // set explicitly: also holds for single-stream handles
+  int vproj_nsplit = 1;              // DDMI_VPROJ_N: 1 = 256-channel tiles + K split, 2 = two 128-channel N halves
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
@@ -292,6 +293,7 @@ class Model {
       vproj_splits_env = true;
     }
     if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 2 ? 2 : 1;
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
     // zeroed on the handle's own stream and waited for: ordered before any forward, on whichever stream it runs
     DD_HIP_CHECK(hipMemsetAsync(in_tab, 0, 4 * sizeof(float*), st_own));
@@ -682,6 +684,7 @@ class Model {
       // device) runs unsplit, which is less work (+0.5 % scenes/s at 3 lanes; one at a time 0.25 ms per forward slower)
       v.max_splits = (use_side || vproj_splits_env) ? vproj_splits : 1;
       v.max_wgs = std::max(64, num_cus() - busy_cus);
+      v.nsplit = vproj_nsplit;
       launch("value_proj", fl, [&] { launch_vproj(v, st); });
       return;
     }

@@ -41,20 +41,33 @@ typedef int vp_i4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kOOBv = 0x80000000u;
 constexpr int kC = 256, kHW = 64;          // channels in / out, BEV map side
-constexpr int VP_WM = 4, VP_WN = 2, VP_TM = 2, VP_TN = 4;
+constexpr int VP_WM = 4, VP_WN = 2, VP_TM = 2;
 constexpr int VP_NW = VP_WM * VP_WN, VP_NT = 64 * VP_NW;
 constexpr int VP_BM = VP_WM * VP_TM * 32;  // 256 rows
-constexpr int VP_BN = VP_WN * VP_TN * 32;  // 256 = every output channel
 constexpr int VP_KC = 32;                  // K chunk
 constexpr int VP_NK = 9 * kC / VP_KC;      // 72 chunks
 constexpr int VP_AB = VP_BM * VP_KC * 4;   // A stage bytes: fp32 rows of 128 B
-constexpr int VP_BB = VP_BN * VP_KC * 2;   // one B image: fp16 rows of 64 B
-constexpr int VP_STAGE = VP_AB + 2 * VP_BB;
 constexpr int VP_A_IN = VP_BM / 8 / VP_NW;   // A DMA instructions per wave per chunk
-constexpr int VP_B_IN = VP_BN / 16 / VP_NW;  // B DMA instructions per wave per chunk and image
-static_assert(2 * VP_STAGE <= 160 * 1024 - 4096, "stages");
-static_assert(VP_A_IN >= 1 && VP_B_IN >= 1, "DMA split over the waves");
+static_assert(VP_A_IN >= 1, "DMA split over the waves");
 static_assert(VP_BM == 256, "the compacted row table holds 256 rows");
+// Tile width: TN = 4 -> 256 output channels (every one; the K split fills the chip), TN = 2 -> 128 (the two N halves
+// of a row tile are two workgroups on one XCD, no K split and no partials)
+template <int TN>
+struct VpTile {
+  static constexpr int BN = VP_WN * TN * 32;
+  static constexpr int BB = BN * VP_KC * 2;  // one B image: fp16 rows of 64 B
+  static constexpr int STAGE = VP_AB + 2 * BB;
+  static constexpr int B_IN = BN / 16 / VP_NW;  // B DMA instructions per wave per chunk and image
+  // LDS stages of the A / B ring: two chunks in flight under the current one's MFMAs where three fit
+  static constexpr int NSTAGE = 3 * STAGE <= 160 * 1024 - 4096 ? 3 : 2;
+  static_assert(2 * STAGE <= 160 * 1024 - 4096, "stages");
+  static_assert(B_IN >= 1, "DMA split over the waves");
+};
+
+template <int N>
+__device__ inline void vp_barrier_n() {  // at most N of this wave's DMAs outstanding, LDS ops retired, barrier
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 
 __device__ inline vp_i4 vp_rsrc(const void* p) {
   const uint64_t a = reinterpret_cast<uint64_t>(p);
@@ -101,8 +114,13 @@ __device__ inline int vp_splits(int tiles, int cap, int budget) {
 
 }  // namespace
 
+template <int VP_TN>
 __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
-  __shared__ __attribute__((aligned(1024))) char lds[2 * VP_STAGE];
+  constexpr int VP_BN = VpTile<VP_TN>::BN, VP_BB = VpTile<VP_TN>::BB, VP_STAGE = VpTile<VP_TN>::STAGE;
+  constexpr int VP_B_IN = VpTile<VP_TN>::B_IN;
+  constexpr int NH = kC / VP_BN;  // N parts of a row tile
+  constexpr int NST = VpTile<VP_TN>::NSTAGE;
+  __shared__ __attribute__((aligned(1024))) char lds[NST * VP_STAGE];
   __shared__ int g_rows[VP_BM];
   __shared__ int g_pre[257];
   __shared__ int g_last;
@@ -113,11 +131,20 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   rowcount_prefix(a.counts, a.B, g_pre);
   const int total = g_pre[a.B];
   const int tiles = (total + VP_BM - 1) / VP_BM;
-  const int S = vp_splits(tiles, a.max_splits, a.max_wgs);
-  const int bid = blockIdx.x;
+  const int S = NH > 1 ? 1 : vp_splits(tiles, a.max_splits, a.max_wgs);
+  int bid = blockIdx.x;
+  int nh = 0;
+  if constexpr (NH > 1) {
+    // the NH halves of row tile m take blocks with equal blockIdx % 8 (one XCD under round-robin placement: the
+    // second half finds the gathered A rows in that XCD's L2; speed only)
+    const int g = bid / (8 * NH), r = bid % (8 * NH);
+    nh = r / 8;
+    bid = g * 8 + r % 8;
+  }
   if (bid >= tiles * S) return;  // workgroup-uniform; touches no counter
   const int mt = bid / S, sp = bid - mt * S;
   const int m0 = mt * VP_BM;
+  const int n0 = nh * VP_BN;
   const int kbeg = sp * VP_NK / S, kend = (sp + 1) * VP_NK / S;
   for (int r = tid; r < VP_BM; r += VP_NT) {
     const int g = m0 + r;
@@ -167,7 +194,7 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   for (int q = 0; q < VP_B_IN; ++q) {
     const int c = b_rbase + q * 16 + (lane >> 2);
     const int slot = (lane & 3) ^ ((c >> 2) & 3);
-    boff[q] = (uint32_t)(c * a.ldh + slot * 8) * 2u;
+    boff[q] = (uint32_t)((n0 + c) * a.ldh + slot * 8) * 2u;
   }
   // chunk ck: tap ck / 8 (kh, kw), channels (ck % 8) * 32 ..
   auto issue = [&](int buf, int ck) {
@@ -214,15 +241,22 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
     }
   }
 
+  // every chunk issues the same DMA count per wave (out-of-range taps read zero through the offset, not skipped)
+  constexpr int DPC = VP_A_IN + 2 * VP_B_IN;
   issue(0, kbeg);
+  if (NST == 3 && kbeg + 1 < kend) issue(1, kbeg + 1);
   int cur = 0;
   for (int kc = kbeg; kc < kend; ++kc) {
-    // this wave's chunk kc has landed, every wave's has (barrier), and every wave finished reading chunk kc - 1,
-    // whose stage is refilled below
-    vp_barrier0();
-    if (kc + 1 < kend) issue(cur ^ 1, kc + 1);
+    // this wave's chunk kc has landed (the younger chunk kc + 1 may stay in flight), every wave's has (barrier),
+    // and every wave finished reading chunk kc - 1, whose stage is refilled below
+    if (NST == 3 && kc + 1 < kend)
+      vp_barrier_n<DPC>();
+    else
+      vp_barrier0();
+    const int nxt = kc + NST - 1;
+    if (nxt < kend) issue(cur == 0 ? NST - 1 : cur - 1, nxt);
     const char* st = lds + cur * VP_STAGE;
-    cur ^= 1;
+    cur = cur + 1 == NST ? 0 : cur + 1;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       vp_h8 ah[VP_TM], al[VP_TM], bh[VP_TN], bl[VP_TN];
@@ -259,7 +293,7 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   float sc[VP_TN], bias[VP_TN];
 #pragma unroll
   for (int j = 0; j < VP_TN; ++j) {
-    const int col = (wn * VP_TN + j) * 32 + li;
+    const int col = n0 + (wn * VP_TN + j) * 32 + li;
     sc[j] = a.wsinv[col];
     bias[j] = a.bias[col];
   }
@@ -276,9 +310,9 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   auto row_of = [&](int i, int r) { return (wm * VP_TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh; };
   auto finish = [&](int i, int j, int r, float v) {
     const int ri = g_rows[row_of(i, r)];
-    if (ri >= 0) a.out[(int64_t)ri * VP_BN + (wn * VP_TN + j) * 32 + li] = fmaxf(v + bias[j], 0.f);
+    if (ri >= 0) a.out[(int64_t)ri * kC + n0 + (wn * VP_TN + j) * 32 + li] = fmaxf(v + bias[j], 0.f);
   };
-  if (S == 1) {
+  if (NH > 1 || S == 1) {
 #pragma unroll
     for (int i = 0; i < VP_TM; ++i)
 #pragma unroll
@@ -287,6 +321,7 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
         for (int r = 0; r < 16; ++r) finish(i, j, r, acc[i][j][r]);
     return;
   }
+  if constexpr (NH > 1) return;
   // ---- this split's partial out, write-through; every storing wave drains before the counter add
   const int64_t MR = (int64_t)a.B * a.cap;
   const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, (int)kOOBv, 0x00020000);
@@ -359,12 +394,18 @@ void launch_vproj(const VprojArgs& a, hipStream_t st) {
   if (!al16(a.map) || !al16(a.wh) || !al16(a.wl) || !al16(a.wsinv) || !al16(a.bias) || !al16(a.part) || !al16(a.out))
     throw std::runtime_error("vproj: operands must be 16-byte aligned");
   // buffer offsets are 32-bit byte offsets below 2^31
-  if ((int64_t)a.B * kHW * kHW * kC * 4 >= (int64_t)kOOBv || (int64_t)3 * a.B * a.cap * VP_BN * 4 >= (int64_t)kOOBv ||
+  if ((int64_t)a.B * kHW * kHW * kC * 4 >= (int64_t)kOOBv || (int64_t)3 * a.B * a.cap * kC * 4 >= (int64_t)kOOBv ||
       (int64_t)kC * a.ldh * 2 >= (int64_t)kOOBv)
     throw std::runtime_error("vproj: operand extent >= 2 GiB");
-  // every (tile, split) the kernel may pick: up to 3 splits of every possible tile
-  const dim3 grid((unsigned)(vproj_tiles(a.B, a.cap) * 3));
-  hipLaunchKernelGGL(vproj_kernel, grid, dim3(VP_NT), 0, st, a);
+  if (a.nsplit == 2) {
+    // two 128-channel halves per row tile, no K split: grid in groups of 8 tiles x 2 halves
+    const size_t t8 = (vproj_tiles(a.B, a.cap) + 7) / 8 * 8;
+    hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, a);
+  } else {
+    // every (tile, split) the kernel may pick: up to 3 splits of every possible tile
+    const dim3 grid((unsigned)(vproj_tiles(a.B, a.cap) * 3));
+    hipLaunchKernelGGL(vproj_kernel<4>, grid, dim3(VP_NT), 0, st, a);
+  }
   DD_HIP_CHECK(hipGetLastError());
 }
 

@@ -471,16 +471,18 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
         gpu_model.set_gemm_mode("fp32")
     runs["splitk2"] = fresh(DDMI_VPROJ_SPLITS="2")
     runs["splitk1"] = fresh(DDMI_VPROJ_SPLITS="1")
+    runs["nhalf2"] = fresh(DDMI_VPROJ_N="2")
     runs["x3"] = fresh(DDMI_VALUE_SPLITK="0")
     runs["x3_per_scene"] = fresh(DDMI_VALUE_SPLITK="0", DDMI_VALUE_COMPACT="0")
     ref_out, ref = runs["x3"]
-    lines = ["== gathered value_proj: value_proj.hip (3 / 2 / 1 splits) vs conv_x3 (compacted / per scene)"]
+    lines = ["== gathered value_proj: value_proj.hip (3 / 2 / 1 K splits; two 128-channel N halves) vs conv_x3 "
+             "(compacted / per scene)"]
     for k in names:
         rows = ref[k][0]
         live = rows >= 0
         assert np.array_equal(rows, runs["x3_per_scene"][1][k][0]), k
         assert np.array_equal(ref[k][1][live], runs["x3_per_scene"][1][k][1][live]), k
-        for v in ("splitk3", "splitk2", "splitk1"):
+        for v in ("splitk3", "splitk2", "splitk1", "nhalf2"):
             got = runs[v][1][k]
             assert np.array_equal(rows, got[0]), (v, k)
             r = ref[k][1][live]
@@ -488,7 +490,7 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
             lines.append(f"  {k} {v}: {int(live.sum())} live rows, max rel err vs conv_x3 {err:.3e}")
             assert err <= 1e-5, (v, k, err)
     assert np.array_equal(ref_out, runs["x3_per_scene"][0])
-    for v in ("splitk3", "splitk2", "splitk1"):
+    for v in ("splitk3", "splitk2", "splitk1", "nhalf2"):
         l2 = waypoint_l2(runs[v][0], ref_out)
         lines.append(f"  trajectory waypoint L2 {v} vs conv_x3 {l2:.3e}")
         assert l2 <= 1e-5, (v, l2)

@@ -6,6 +6,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
 i=0
 for cfg in "$@" "$1"; do
   i=$((i+1))
-  env $cfg timeout -k 10 200 python bench.py --steps ${STEPS:-100} --no-cpu-baseline --no-compare > gpurun_out/envab_$i.log 2>&1 || { tail -5 gpurun_out/envab_$i.log; exit 1; }
+  env $cfg timeout -k 10 200 python bench.py --steps ${STEPS:-100} --no-cpu-baseline --no-compare ${BENCH_EXTRA:-} > gpurun_out/envab_$i.log 2>&1 || { tail -5 gpurun_out/envab_$i.log; exit 1; }
   python -c "import json;d=json.loads(open('gpurun_out/envab_$i.log').read().strip().splitlines()[-1]);dm=d['device_ms_per_step'];print('[$cfg]', d['value'], d['ms_per_step'], {k: round(v,3) for k,v in dm.items()})"
 done
