@@ -61,8 +61,8 @@ def agent_loss(targets: Dict, predictions: Dict, config: TransfuserConfig):
 
 def bev_semantic_loss(model, logits: torch.Tensor, target) -> torch.Tensor:
     """F.cross_entropy(bev_semantic_map, target.long()) on the GPU (dd_bev_semantic_loss)."""
-    if not isinstance(logits, torch.Tensor) or logits.device.type != "cuda":
-        raise _lib.DDMIError("bev_semantic_loss needs the device bev_semantic_map of the forward")
+    # eval-mode predictions come back on the CPU (the reference's contract); the loss runs on the model's device
+    logits = torch.as_tensor(logits).to(device=f"cuda:{model.device}", dtype=torch.float32)
     B, C, H, W = logits.shape
     tg = torch.as_tensor(target)
     if tuple(tg.shape) != (B, H, W):
