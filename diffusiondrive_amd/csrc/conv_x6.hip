@@ -81,14 +81,17 @@ __device__ inline x6f4 vload6(x6i4 rsrc, uint32_t voff) {
   return v;
 }
 
-// wait until at most N vector-memory ops of this wave are outstanding, then LDS ops, then barrier
-template <int N>
+// wait until at most N vector-memory ops of this wave are outstanding, then (LGKM) its LDS ops, then barrier
+template <int N, bool LGKM = true>
 __device__ inline void step_barrier() {
   static_assert(N >= 0 && N < 64, "vmcnt");
 #ifdef DDMI_X6_NOBAR  // timing diagnostic only (variant build x6nb): races by construction
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
 #else
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  if constexpr (LGKM)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 #endif
 }
 
@@ -388,7 +391,11 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
     constexpr int N = (D - 1) * BPS + (halo_in_window(t, D, TA, first) ? ALD : 0);
-    step_barrier<N>();
+    // the barrier opening step s refills slot (s + D) % NSLOT. With NSLOT = D + 1 that is the slot of step s - 1,
+    // whose second-half fragment reads were issued just before: they must have returned (lgkmcnt(0)) before any
+    // wave's DMA may overwrite it. With NSLOT >= D + 2 it is the slot of step s - 2, which every wave's MFMAs
+    // already consumed before this barrier, so the fragment reads just issued stay in flight across it.
+    step_barrier<N, (NSLOT < D + 2) || t == 0>();  // t == 0: the chunk's halo stores must have landed too
     constexpr int tn = (t + D) % 9;
     int ns = slot + D;
     if (ns >= NSLOT) ns -= NSLOT;
@@ -608,6 +615,14 @@ static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
   launch_x6_nt<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
 }
 
+// A spare B-ring slot (NSLOT >= D + 2) lets each step's second-half fragment reads stay in flight across the next
+// barrier (step_barrier without lgkmcnt(0)): the BN = 128 forms at 4 slots then prefetch 2 steps ahead instead of 3,
+// the 8-wave BN = 64 forms take a 4th slot, the 8 x 8 form a 5th (DDMI_X6_RELAX=1, read per dispatch; A/B)
+static bool x6_relax() {
+  const char* e = getenv("DDMI_X6_RELAX");
+  return e && atoi(e) == 1;
+}
+
 // Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 / bf16 conv this kernel covers (the
 // caller then takes conv_x5 / conv_x3).
 bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
@@ -629,7 +644,7 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // the CUs idle, measured 72 us against 61: the 10 x 10 halo per 64 pixels costs more than the idle CUs.)
   if (a.Ho == 8 && a.Wo == 8 && a.Cout % 128 == 0) {
     if ((int64_t)a.Nimg * (a.Cout / 128) < 128) return false;
-    launch_x6_cfg<8, 8, 128, 2, 4, 3, 4, 0>(a, st);
+    if (x6_relax()) launch_x6_cfg<8, 8, 128, 2, 4, 3, 5, 0>(a, st); else launch_x6_cfg<8, 8, 128, 2, 4, 3, 4, 0>(a, st);
     return true;
   }
   const bool wide = a.Ho < 16;  // 8 x 32 tiles for the 8-row maps (layer4 of the image trunk)
@@ -652,15 +667,15 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   if (wide) {
     if (b128) {
-      X6(8, 32, 128, 4, 2, 3, 4, 0);
+      if (x6_relax()) X6(8, 32, 128, 4, 2, 2, 4, 0); else X6(8, 32, 128, 4, 2, 3, 4, 0);
     } else {
-      if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else X6(8, 32, 64, 4, 2, 2, 3, 0);
+      if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else if (x6_relax()) X6(8, 32, 64, 4, 2, 2, 4, 0); else X6(8, 32, 64, 4, 2, 2, 3, 0);
     }
   } else {
     if (b128) {
-      X6(16, 16, 128, 4, 2, 3, 4, 0);
+      if (x6_relax()) X6(16, 16, 128, 4, 2, 2, 4, 0); else X6(16, 16, 128, 4, 2, 3, 4, 0);
     } else {
-      if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else X6(16, 16, 64, 4, 2, 2, 3, 0);
+      if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else if (x6_relax()) X6(16, 16, 64, 4, 2, 2, 4, 0); else X6(16, 16, 64, 4, 2, 2, 3, 0);
     }
   }
 #undef X6
