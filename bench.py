@@ -90,8 +90,8 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="scenes per GPU")
     p.add_argument("--denoise-steps", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", default="", help="extra thread counts of the CPU-oracle baseline (1 rep each; "
-                                                      "the job's CPU share always runs, 3 reps)")
+    p.add_argument("--cpu-threads", default="8", help="extra thread counts of the CPU-oracle baseline beside the job's "
+                                                       "CPU share (BASELINE.md: n = 8 and n = all cores; 3 reps each)")
     p.add_argument("--arch", default="resnet34")
     p.add_argument("--gemm", default="f16x3", choices=["fp32", "f16x3", "bf16"],
                    help="conv/linear arithmetic: fp32 MFMA, the fp32-class 3-product fp16 split, or bf16")
@@ -521,7 +521,7 @@ def cpu_share():
 
 def cpu_baseline(args, cfg, sd, inp):
     """Golden-pinned CPU oracle timed on this host at the job's CPU share (cpu_share): B = 64 (the metric's
-    batch, 3 timed reps after a B = 1 warm-up) and B = 1 (3 reps); --cpu-threads adds other thread counts.
+    batch, 3 timed reps after an untimed B = 1 and B = 64 warm-up) and B = 1 (3 reps); --cpu-threads adds thread counts.
     Returns (record, oracle trajectories of the B = 64 sample)."""
     from oracle.model import OracleModel
     om = OracleModel(sd, cfg)
@@ -535,14 +535,16 @@ def cpu_baseline(args, cfg, sd, inp):
     share, share_src = cpu_share()
     threads = [share] + [int(t) for t in args.cpu_threads.split(",") if t and int(t) != share]
     grid, ref = {}, None
-    for n_t in threads:
+    for i_t, n_t in enumerate(threads):
         torch.set_num_threads(n_t)
         run(1)  # warm-up
+        if i_t == 0:
+            ref = run(S)  # warm-up of the batch shape (first-touch allocations); its result is the parity reference
         t0 = time.perf_counter()
         for _ in range(REPS):
             run(1)
         b1 = REPS / (time.perf_counter() - t0)
-        reps = REPS if n_t == share else 1
+        reps = REPS
         times = []
         for _ in range(reps):
             t0 = time.perf_counter()
