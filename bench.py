@@ -62,7 +62,7 @@ CANONICAL_GFLOP_PER_SCENE_2STEP = 65.27  # SURVEY.md §8d (value_proj once per l
 FP32_MFMA_PEAK_TFLOPS = 157.3            # MI355X dense fp32 MFMA (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0            # MI355X dense f16 / bf16 MFMA peak (no sparsity)
 # measured whole-chip f16 32x32x16 MFMA loop on random operands (clock held ~1.55 GHz under DVFS):
-# profiles/round2_h_mfma_shape.txt (tools/micro/mfma_shape.hip) - the rate a real kernel can sustain
+# profiles/archive/round2_h_mfma_shape.txt (tools/micro/mfma_shape.hip) - the rate a real kernel can sustain
 F16_MFMA_SUSTAINED_TFLOPS = 1600.0
 # peak of ALGORITHMIC FLOPs per gemm mode: f16x3 issues 3 f16 MFMA products per fp32 MAC
 ALGO_PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16x3": F16_MFMA_PEAK_TFLOPS / 3, "bf16": F16_MFMA_PEAK_TFLOPS}
@@ -384,7 +384,7 @@ def main():
             "frac_of_sustained": round(achieved / (F16_MFMA_SUSTAINED_TFLOPS / (3.0 if args.gemm == "f16x3" else 1.0)), 4)
             if args.gemm != "fp32" else None,
             "sustained_note": "measured f16 32x32x16 MFMA loop on random data, whole chip: 1600 TF "
-                              "(profiles/round2_h_mfma_shape.txt); peak/frac stay on the nominal ceiling",
+                              "(profiles/archive/round2_h_mfma_shape.txt); peak/frac stay on the nominal ceiling",
             "traffic": traffic,
             "traffic_source": (f"{os.path.relpath(pmc_path, ROOT)} (measured {pmc_meta.get('measured', '?')}, "
                                f"{pmc_meta.get('source', '?')})") if traffic is not None else None,
