@@ -158,7 +158,7 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // NTL: cache policy of the activation streams (DDMI_X6_NT, read per dispatch): bit 0 = the halo loads nontemporal,
 // bit 1 = the epilogue's residual loads nontemporal.
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC, int NTL>
-__global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
+__global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks, int diag) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = TH * TW;
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   // hofs: element offset of (pixel, 4q) at chunk 0, or -1 (zero fill); hwad: LDS byte offset (in a
   // halo buffer) of the hi 8 bytes (bf16: of the quad's 8 bytes), -1 = no write. Kept in registers for
   // 8-wave workgroups, recomputed per use by 4-wave ones (ALD = 11), whose register file is the limit.
-  constexpr bool HKEEP = NW == 8 && ALD <= 12;
+  constexpr bool HKEEP = NW == 8 && ALD <= 12 && !SH;
   auto hofs_of = [&](int i) {
     const int e = tid + NT * i;
     const int px = e / QP, q = e % QP;
@@ -325,6 +325,10 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // PIPE: each half-step's fragment reads are issued under the previous half-step's MFMAs (two fragment sets in
+  // registers). The two-per-CU 8-wave form (128 VGPRs) keeps one set: reads, then their MFMAs - its partner waves
+  // (four per SIMD) cover the LDS latency.
+  constexpr bool PIPE = !(SH && NW == 8);
   // fragments of one k16 half-step: F0 = (step, s2 = 0), F1 = (step, s2 = 1)
   struct Frag {
     x6h8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -395,7 +399,9 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
     // whose second-half fragment reads were issued just before: they must have returned (lgkmcnt(0)) before any
     // wave's DMA may overwrite it. With NSLOT >= D + 2 it is the slot of step s - 2, which every wave's MFMAs
     // already consumed before this barrier, so the fragment reads just issued stay in flight across it.
-    step_barrier<N, (NSLOT < D + 2) || t == 0>();  // t == 0: the chunk's halo stores must have landed too
+    // t == 0: the chunk's halo stores must have landed too. Unpipelined (PIPE false): every read of the previous
+    // steps was consumed by this wave's MFMAs before the barrier, so only the halo stores need the wait.
+    step_barrier<N, (PIPE && NSLOT < D + 2) || t == 0>();
     constexpr int tn = (t + D) % 9;
     int ns = slot + D;
     if (ns >= NSLOT) ns -= NSLOT;
@@ -411,7 +417,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   halo_tie();
   halo_store(0);
   open_step(0, std::integral_constant<int, 0>(), std::true_type());
-  load_frag(F0, 0, 0, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+  if constexpr (PIPE) load_frag(F0, 0, 0, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
 
   // step (c, t), software pipelined: [F1 reads] [MFMAs F0] [(t == 8) halo c+1 -> other buffer]
   // [open step s+1] [F0 reads of s+1] [MFMAs F1]: every fragment read is in flight under the
@@ -419,6 +425,23 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   auto step = [&](int c, auto TAP, auto FIRST) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
+    if constexpr (!PIPE) {
+      load_frag(F0, slot, c, TAP, std::integral_constant<int, 0>());
+      mfma_frag(F0);
+      load_frag(F0, slot, c, TAP, std::integral_constant<int, 1>());
+      mfma_frag(F0);
+      if constexpr (t == 8) {
+        wait_vm<(8 - TA) * BPS>();
+        halo_tie();
+        // every wave's MFMAs (hence fragment reads) of this chunk's halo are behind it
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        halo_store(0);
+      }
+      if (++slot == NSLOT) slot = 0;
+      open_step(t == 8 ? c + 1 : c, std::integral_constant<int, (t + 1) % 9>(),
+                std::integral_constant<bool, first && t != 8>());
+      return;
+    }
     load_frag(F1, slot, c, TAP, std::integral_constant<int, 1>());
     __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs they overlap
     mfma_frag(F0);
@@ -479,7 +502,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   constexpr int IT = BM / (NT / QN);  // pixels per thread
   // (8-wave workgroups: up to 16 quads - the fragment / halo registers are dead by now; ~1 % on the BN = 128
   // layers, same-box A/B)
-  constexpr bool EARLY = IT <= (NW == 8 ? 16 : 8);
+  constexpr bool EARLY = IT <= (NW == 8 && !SH ? 16 : 8) && !(SH && NW == 8);
   x6f4 rv[IT];
   int ooff[IT];
   auto load_res = [&]() {
@@ -658,13 +681,21 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // chunk would double the 4-wave form's staging registers)
   bool sh4 = a.prec == 0 && a.Cin <= 64;
   bool b128 = bn128;
+  bool sh8 = false;  // DDMI_X6_CFG = 3: BN = 128 as 8-wave workgroups on 8 x 16 tiles, one halo buffer, two per CU
   // micro-benchmark override, read per dispatch: DDMI_X6_CFG = 1 forces the 4-wave BN = 64 form, 2 the 8-wave BN = 64 form
   if (const char* ce = getenv("DDMI_X6_CFG")) {
     const int cf = atoi(ce);
     if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
     if (cf == 2) { sh4 = false; b128 = false; }
+    if (cf == 3 && b128 && a.prec == 0) sh8 = true;
   }
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
+  if (sh8) {
+    // 8 x 16 pixels x 128 channels: 23 KB halo + 3 x 16 KB ring (71 KB), wave tile 32 x 64 (<= 128 VGPRs): two
+    // workgroups per CU, four waves per SIMD, one's prologue / epilogue beside the other's K loop
+    X6(8, 16, 128, 4, 2, 2, 3, 1);
+    return true;
+  }
   if (wide) {
     if (b128) {
       if (x6_relax()) X6(8, 32, 128, 4, 2, 2, 4, 0); else X6(8, 32, 128, 4, 2, 3, 4, 0);

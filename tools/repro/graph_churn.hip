@@ -4,10 +4,13 @@
 // hand-off from the caller's stream, or single-stream directly on a long-lived caller stream), replayed, then the
 // handle torn down in runtime.cpp ~Model's order (sync, exec destroy, events, streams, buffer).
 //
-//   graph_churn <iterations> <pool 0|1> <kernels per branch>
+//   graph_churn <iterations> <pool 0|1> <kernels per branch> [all 0|1]
 //
 // pool 1 keeps destroyed handles' streams for the next handles (runtime.cpp's process-wide pool), pool 0 destroys
-// them. Prints one line per 25 iterations; a segfault ends the process (the driving script reports the exit code).
+// them. all 1: no stream outlives an iteration (the caller streams and the long-lived handle are re-created every
+// iteration too), so the runtime's hardware queues - GPU_MAX_HW_QUEUES, shared round-robin by streams - can be
+// released and re-created between handles. Prints one line per 25 iterations; a segfault ends the process (the
+// driving script reports the exit code).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -122,11 +125,19 @@ int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 200;
   g_pool = argc > 2 ? atoi(argv[2]) != 0 : true;
   const int K = argc > 3 ? atoi(argv[3]) : 64;
+  const bool all = argc > 4 && atoi(argv[4]) != 0;
   CK(hipSetDevice(0));
   hipStream_t callers[3];
   for (auto& s : callers) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));  // torch's pooled streams
   Handle* keep = new Handle(false, K);  // a long-lived two-stream handle (the tests' module-scoped model)
   for (int i = 0; i < iters; ++i) {
+    if (all && i > 0) {  // nothing outlives the iteration: every stream of the process is re-created
+      delete keep;
+      for (auto& s : callers) CK(hipStreamDestroy(s));
+      CK(hipDeviceSynchronize());
+      for (auto& s : callers) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      keep = new Handle(false, K);
+    }
     {  // three lanes in flight: the first a two-stream handle on the null stream, two single-stream clones
       Handle a(false, K), b(true, K), c(true, K);
       for (int r = 0; r < 4; ++r) {
@@ -149,6 +160,7 @@ int main(int argc, char** argv) {
   }
   delete keep;
   for (auto& s : callers) CK(hipStreamDestroy(s));
-  std::printf("graph_churn: %d iterations, pool %d, %d kernels per branch: no fault\n", iters, (int)g_pool, K);
+  std::printf("graph_churn: %d iterations, pool %d, %d kernels per branch, all %d: no fault\n", iters, (int)g_pool, K,
+              (int)all);
   return 0;
 }
