@@ -199,7 +199,10 @@ class Model {
   bool value_splitk = true;          // DDMI_VALUE_SPLITK=0: the gathered value_proj on conv_x3 (one launch, K whole)
   int vproj_splits = 3;              // DDMI_VPROJ_SPLITS: most K splits of value_proj.hip (1..3)
   bool vproj_splits_env = false;     // set explicitly: also holds for single-stream handles
-  int vproj_nsplit = 1;              // DDMI_VPROJ_N: 1 = 256-channel tiles + K split, 2 = two 128-channel N halves
+  // DDMI_VPROJ_N: 2 (default) = two 128-channel N halves per row tile, no K split (no partials; exact, equal to the
+  // unsplit sum); 1 = 256-channel tiles with the K split (one at a time 4972-5017 -> 5109 scenes/s with 2, 3 in
+  // flight unchanged: profiles/round4_d_envab_if1.txt)
+  int vproj_nsplit = 2;
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
@@ -293,7 +296,7 @@ class Model {
       vproj_splits_env = true;
     }
     if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 2 ? 2 : 1;
+    if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
     // zeroed on the handle's own stream and waited for: ordered before any forward, on whichever stream it runs
     DD_HIP_CHECK(hipMemsetAsync(in_tab, 0, 4 * sizeof(float*), st_own));

@@ -425,12 +425,13 @@ def test_fused_token_pooling_matches_avgpool(gpu_model, seeded_sd, monkeypatch):
 
 
 def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
-    """The gathered value_proj on the same inputs: the default kernel (value_proj.hip: compacted rows in 256 x 256
-    tiles, K split up to three ways, the partials summed in split order by the last split), the same kernel held to
-    two and to one split (DDMI_VPROJ_SPLITS), conv_x3 over the compacted rows (DDMI_VALUE_SPLITK=0) and conv_x3
-    with one tile run per scene (+ DDMI_VALUE_COMPACT=0). The two conv_x3 forms evaluate every row with the same
-    dot products in the same K order wherever its tile sits: bit-identical. value_proj.hip differs from them by
-    summation order only: every live row within 1e-5 relative, trajectories within 1e-5."""
+    """The gathered value_proj on the same inputs: the default kernel (value_proj.hip: compacted rows in 256-row
+    tiles, each tile as two 128-channel halves, K whole), its 256 x 256 form with the K split three / two / one ways
+    (DDMI_VPROJ_N=1, DDMI_VPROJ_SPLITS; the partials summed in split order by the last split), conv_x3 over the
+    compacted rows (DDMI_VALUE_SPLITK=0) and conv_x3 with one tile run per scene (+ DDMI_VALUE_COMPACT=0). The
+    conv_x3 forms evaluate every row with the same dot products in the same K order wherever its tile sits:
+    bit-identical, and so are the unsplit value_proj.hip forms. The K-split forms differ by summation order only:
+    every live row within 1e-5 relative, trajectories within 1e-5."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
     B = 6
@@ -465,13 +466,13 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
 
     gpu_model.set_gemm_mode("f16x3")
     try:
-        runs = {"splitk3": run(gpu_model, profile=True)}
+        runs = {"nhalf2": run(gpu_model, profile=True)}  # the default: two 128-channel halves, no K split
     finally:
         gpu_model.set_profiling(False)
         gpu_model.set_gemm_mode("fp32")
-    runs["splitk2"] = fresh(DDMI_VPROJ_SPLITS="2")
-    runs["splitk1"] = fresh(DDMI_VPROJ_SPLITS="1")
-    runs["nhalf2"] = fresh(DDMI_VPROJ_N="2")
+    runs["splitk3"] = fresh(DDMI_VPROJ_N="1")
+    runs["splitk2"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="2")
+    runs["splitk1"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="1")
     runs["x3"] = fresh(DDMI_VALUE_SPLITK="0")
     runs["x3_per_scene"] = fresh(DDMI_VALUE_SPLITK="0", DDMI_VALUE_COMPACT="0")
     ref_out, ref = runs["x3"]
