@@ -71,27 +71,20 @@ __device__ inline void dma6(x6i4 rsrc, uint32_t lds_wave, uint32_t voff) {
                : "memory");
 }
 
-template <int NTL>
 __device__ inline x6f4 vload6(x6i4 rsrc, uint32_t voff) {
   x6f4 v;
-  if constexpr (NTL)  // nontemporal: the streamed activation halo does not displace the weight slices in L2
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
-  else
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
   return v;
 }
 
-// wait until at most N vector-memory ops of this wave are outstanding, then (LGKM) its LDS ops, then barrier
-template <int N, bool LGKM = true>
+// wait until at most N vector-memory ops of this wave are outstanding, then LDS ops, then barrier
+template <int N>
 __device__ inline void step_barrier() {
   static_assert(N >= 0 && N < 64, "vmcnt");
 #ifdef DDMI_X6_NOBAR  // timing diagnostic only (variant build x6nb): races by construction
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
 #else
-  if constexpr (LGKM)
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 #endif
 }
 
@@ -155,10 +148,8 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // PREC 0: f16x3 (32-channel chunks; a halo pixel row / B slot holds the hi and lo fp16 images of them);
 // PREC 1: bf16 (64-channel chunks; the same bytes hold channels 0-31 and 32-63 of the chunk in bf16, and
 // each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
-// NTL: cache policy of the activation streams (DDMI_X6_NT, read per dispatch): bit 0 = the halo loads nontemporal,
-// bit 1 = the epilogue's residual loads nontemporal.
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC, int NTL>
-__global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
+__global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks, int diag) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = TH * TW;
@@ -215,7 +206,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
   // hofs: element offset of (pixel, 4q) at chunk 0, or -1 (zero fill); hwad: LDS byte offset (in a
   // halo buffer) of the hi 8 bytes (bf16: of the quad's 8 bytes), -1 = no write. Kept in registers for
   // 8-wave workgroups, recomputed per use by 4-wave ones (ALD = 11), whose register file is the limit.
-  constexpr bool HKEEP = NW == 8 && ALD <= 12 && !SH;
+  constexpr bool HKEEP = NW == 8 && ALD <= 12;
   auto hofs_of = [&](int i) {
     const int e = tid + NT * i;
     const int px = e / QP, q = e % QP;
@@ -246,7 +237,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
 #pragma unroll
     for (int i = 0; i < ALD; ++i) {
       const int ho = HKEEP ? hofs[HKEEP ? i : 0] : hofs_of(i);
-      hr[i] = vload6<NTL & 1>(rin, (cv && ho >= 0) ? (uint32_t)(ho + co) * 4u : kOOB6);
+      hr[i] = vload6(rin, (cv && ho >= 0) ? (uint32_t)(ho + co) * 4u : kOOB6);
     }
   };
   auto halo_tie = [&]() {  // after a wait: no use of the staged registers may move above it
@@ -325,10 +316,6 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // PIPE: each half-step's fragment reads are issued under the previous half-step's MFMAs (two fragment sets in
-  // registers). The two-per-CU 8-wave form (128 VGPRs) keeps one set: reads, then their MFMAs - its partner waves
-  // (four per SIMD) cover the LDS latency.
-  constexpr bool PIPE = !(SH && NW == 8);
   // fragments of one k16 half-step: F0 = (step, s2 = 0), F1 = (step, s2 = 1)
   struct Frag {
     x6h8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -395,13 +382,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
     constexpr int N = (D - 1) * BPS + (halo_in_window(t, D, TA, first) ? ALD : 0);
-    // the barrier opening step s refills slot (s + D) % NSLOT. With NSLOT = D + 1 that is the slot of step s - 1,
-    // whose second-half fragment reads were issued just before: they must have returned (lgkmcnt(0)) before any
-    // wave's DMA may overwrite it. With NSLOT >= D + 2 it is the slot of step s - 2, which every wave's MFMAs
-    // already consumed before this barrier, so the fragment reads just issued stay in flight across it.
-    // t == 0: the chunk's halo stores must have landed too. Unpipelined (PIPE false): every read of the previous
-    // steps was consumed by this wave's MFMAs before the barrier, so only the halo stores need the wait.
-    step_barrier<N, (PIPE && NSLOT < D + 2) || t == 0>();
+    step_barrier<N>();
     constexpr int tn = (t + D) % 9;
     int ns = slot + D;
     if (ns >= NSLOT) ns -= NSLOT;
@@ -417,7 +398,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
   halo_tie();
   halo_store(0);
   open_step(0, std::integral_constant<int, 0>(), std::true_type());
-  if constexpr (PIPE) load_frag(F0, 0, 0, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+  load_frag(F0, 0, 0, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
 
   // step (c, t), software pipelined: [F1 reads] [MFMAs F0] [(t == 8) halo c+1 -> other buffer]
   // [open step s+1] [F0 reads of s+1] [MFMAs F1]: every fragment read is in flight under the
@@ -425,23 +406,6 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
   auto step = [&](int c, auto TAP, auto FIRST) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
-    if constexpr (!PIPE) {
-      load_frag(F0, slot, c, TAP, std::integral_constant<int, 0>());
-      mfma_frag(F0);
-      load_frag(F0, slot, c, TAP, std::integral_constant<int, 1>());
-      mfma_frag(F0);
-      if constexpr (t == 8) {
-        wait_vm<(8 - TA) * BPS>();
-        halo_tie();
-        // every wave's MFMAs (hence fragment reads) of this chunk's halo are behind it
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        halo_store(0);
-      }
-      if (++slot == NSLOT) slot = 0;
-      open_step(t == 8 ? c + 1 : c, std::integral_constant<int, (t + 1) % 9>(),
-                std::integral_constant<bool, first && t != 8>());
-      return;
-    }
     load_frag(F1, slot, c, TAP, std::integral_constant<int, 1>());
     __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs they overlap
     mfma_frag(F0);
@@ -502,7 +466,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
   constexpr int IT = BM / (NT / QN);  // pixels per thread
   // (8-wave workgroups: up to 16 quads - the fragment / halo registers are dead by now; ~1 % on the BN = 128
   // layers, same-box A/B)
-  constexpr bool EARLY = IT <= (NW == 8 && !SH ? 16 : 8) && !(SH && NW == 8);
+  constexpr bool EARLY = IT <= (NW == 8 ? 16 : 8);
   x6f4 rv[IT];
   int ooff[IT];
   auto load_res = [&]() {
@@ -512,11 +476,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
       const int oy = oy0 + p / TW, ox = ox0 + p % TW;
       const bool ok = nv && oy < a.Ho && ox < a.Wo;
       ooff[k] = ok ? oy * osh + ox * osw : -1;
-      rv[k] = (x6f4){0.f, 0.f, 0.f, 0.f};
-      if (res && ok) {
-        const x6f4* rp = reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw));
-        rv[k] = (NTL & 2) ? __builtin_nontemporal_load(rp) : *rp;
-      }
+      rv[k] = (res && ok) ? *reinterpret_cast<const x6f4*>(res + (oy * rsh + ox * rsw)) : (x6f4){0.f, 0.f, 0.f, 0.f};
     }
   };
   if constexpr (EARLY) load_res();
@@ -586,7 +546,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void
 #endif
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC, int NTL>
+template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
 static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
   ConvArgs a = a_in;
   // fused token pooling: whole tiles only, windows inside tiles, 16-B aligned channel quads
@@ -608,42 +568,21 @@ static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
   // read, bit 1 = skip the output store (WRONG results; tools/gpu_x6exp.sh)
   const char* de = getenv("DDMI_X6_DIAG");
   const int diag = de ? atoi(de) : 0;
-  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, NTL>), dim3(n_sp * ntn), dim3(64 * WM * WN),
-                     0, st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
+  hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0,
+                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
   DD_HIP_CHECK(hipGetLastError());
-}
-static int x6_nt() {
-  const char* e = getenv("DDMI_X6_NT");
-  return e ? atoi(e) & 3 : 0;
-}
-template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
-static void launch_x6_nt(const ConvArgs& a, hipStream_t st) {
-  switch (x6_nt()) {
-    case 1: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 1>(a, st); break;
-    case 2: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 2>(a, st); break;
-    case 3: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 3>(a, st); break;
-    default: launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC, 0>(a, st); break;
-  }
 }
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
 static void launch_x6_cfg(const ConvArgs& a, hipStream_t st) {
   if constexpr (SH == 0) {
     if (a.prec == 1) {
-      launch_x6_nt<TH, TW, BN, WM, WN, D, NSLOT, SH, 1>(a, st);
+      launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 1>(a, st);
       return;
     }
   } else {
     if (a.prec == 1) throw std::runtime_error("conv_x6: bf16 takes the 8-wave configurations");
   }
-  launch_x6_nt<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
-}
-
-// A spare B-ring slot (NSLOT >= D + 2) lets each step's second-half fragment reads stay in flight across the next
-// barrier (step_barrier without lgkmcnt(0)): the BN = 128 forms at 4 slots then prefetch 2 steps ahead instead of 3,
-// the 8-wave BN = 64 forms take a 4th slot, the 8 x 8 form a 5th (DDMI_X6_RELAX=1, read per dispatch; A/B)
-static bool x6_relax() {
-  const char* e = getenv("DDMI_X6_RELAX");
-  return e && atoi(e) == 1;
+  launch_x6_one<TH, TW, BN, WM, WN, D, NSLOT, SH, 0>(a, st);
 }
 
 // Returns false when the conv is not a 3x3 / stride 1 / pad 1 f16x3 / bf16 conv this kernel covers (the
@@ -667,7 +606,7 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // the CUs idle, measured 72 us against 61: the 10 x 10 halo per 64 pixels costs more than the idle CUs.)
   if (a.Ho == 8 && a.Wo == 8 && a.Cout % 128 == 0) {
     if ((int64_t)a.Nimg * (a.Cout / 128) < 128) return false;
-    if (x6_relax()) launch_x6_cfg<8, 8, 128, 2, 4, 3, 5, 0>(a, st); else launch_x6_cfg<8, 8, 128, 2, 4, 3, 4, 0>(a, st);
+    launch_x6_cfg<8, 8, 128, 2, 4, 3, 4, 0>(a, st);
     return true;
   }
   const bool wide = a.Ho < 16;  // 8 x 32 tiles for the 8-row maps (layer4 of the image trunk)
@@ -681,32 +620,24 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // chunk would double the 4-wave form's staging registers)
   bool sh4 = a.prec == 0 && a.Cin <= 64;
   bool b128 = bn128;
-  bool sh8 = false;  // DDMI_X6_CFG = 3: BN = 128 as 8-wave workgroups on 8 x 16 tiles, one halo buffer, two per CU
   // micro-benchmark override, read per dispatch: DDMI_X6_CFG = 1 forces the 4-wave BN = 64 form, 2 the 8-wave BN = 64 form
   if (const char* ce = getenv("DDMI_X6_CFG")) {
     const int cf = atoi(ce);
     if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
     if (cf == 2) { sh4 = false; b128 = false; }
-    if (cf == 3 && b128 && a.prec == 0) sh8 = true;
   }
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
-  if (sh8) {
-    // 8 x 16 pixels x 128 channels: 23 KB halo + 3 x 16 KB ring (71 KB), wave tile 32 x 64 (<= 128 VGPRs): two
-    // workgroups per CU, four waves per SIMD, one's prologue / epilogue beside the other's K loop
-    X6(8, 16, 128, 4, 2, 2, 3, 1);
-    return true;
-  }
   if (wide) {
     if (b128) {
-      if (x6_relax()) X6(8, 32, 128, 4, 2, 2, 4, 0); else X6(8, 32, 128, 4, 2, 3, 4, 0);
+      X6(8, 32, 128, 4, 2, 3, 4, 0);
     } else {
-      if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else if (x6_relax()) X6(8, 32, 64, 4, 2, 2, 4, 0); else X6(8, 32, 64, 4, 2, 2, 3, 0);
+      if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else X6(8, 32, 64, 4, 2, 2, 3, 0);
     }
   } else {
     if (b128) {
-      if (x6_relax()) X6(16, 16, 128, 4, 2, 2, 4, 0); else X6(16, 16, 128, 4, 2, 3, 4, 0);
+      X6(16, 16, 128, 4, 2, 3, 4, 0);
     } else {
-      if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else if (x6_relax()) X6(16, 16, 64, 4, 2, 2, 4, 0); else X6(16, 16, 64, 4, 2, 2, 3, 0);
+      if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else X6(16, 16, 64, 4, 2, 2, 3, 0);
     }
   }
 #undef X6
