@@ -453,9 +453,13 @@ def value_proj_record(model, vp, prof_steps, B, args):
     if not vp["launches"]:
         return None
     live = 0
+    algo_bytes = []
     for s in range(args.denoise_steps):
         for l in range(2):
-            live += int(model.tap(f"value_cnt_s{s}l{l}")[:B].view(torch.int32).sum().item())
+            cnt = model.tap(f"value_cnt_s{s}l{l}")[:B].view(torch.int32).cpu().numpy()
+            live += int(cnt.sum())
+            algo_bytes.append(value_proj_algo_bytes(model.tap(f"value_taps_s{s}l{l}").view(torch.int32).cpu().numpy(),
+                                                    cnt, B))
     per_launch_live = live / (2 * args.denoise_steps)
     live_flops = 2.0 * live * 256 * 2304 * prof_steps
     sec = vp["ms"] * 1e-3
@@ -466,8 +470,28 @@ def value_proj_record(model, vp, prof_steps, B, args):
             "live_tflops": round(live_tf, 2),
             "live_frac_of_f16x3_ceiling": round(live_tf / ALGO_PEAK["f16x3"], 4),
             "live_mfma_equiv_util": round(live_tf * 3 / F16_MFMA_SUSTAINED_TFLOPS, 4),
+            "algorithmic_bytes_per_launch": round(float(np.mean(algo_bytes))),
             "note": "live_mfma_equiv_util = live-row f16 MFMA FLOP rate (3 products per MAC) / the measured sustained "
-                    "whole-chip f16 MFMA rate; the PMC MFMA-busy of the same launches is in profiles/"}
+                    "whole-chip f16 MFMA rate; the PMC MFMA-busy of the same launches is in profiles/. "
+                    "algorithmic_bytes_per_launch: the distinct map pixels of the live rows' 3x3 neighbourhoods "
+                    "(1 KB each) + the live output rows (1 KB each) + the split weight image (2304 x 256 x 4 B), "
+                    "averaged over the forward's launches"}
+
+
+def value_proj_algo_bytes(taps, counts, B, hw=64, C=256):
+    """Algorithmic HBM bytes of one gathered value_proj launch: every map pixel some live row's 3x3 neighbourhood
+    covers, read once; every live output row written once; the f16x3 weight image (hi + lo fp16) read once. ``taps``
+    holds each scene's distinct pixel indices (n * hw * hw + y * hw + x) at [b * cap, b * cap + counts[b])."""
+    cap = taps.size // B
+    px = np.concatenate([taps[b * cap:b * cap + int(counts[b])] for b in range(B)]).astype(np.int64)
+    n, y, x = px // (hw * hw), (px // hw) % hw, px % hw
+    cover = set()
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            yy, xx = y + dy, x + dx
+            ok = (yy >= 0) & (yy < hw) & (xx >= 0) & (xx < hw)
+            cover.update(((n * hw + yy) * hw + xx)[ok].tolist())
+    return (len(cover) + px.size) * C * 4 + 9 * C * C * 4
 
 
 def completion_intervals(e_start, marks, lanes):
