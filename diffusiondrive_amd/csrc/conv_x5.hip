@@ -75,13 +75,6 @@ __device__ inline void chunk_barrier() {
 #endif
 }
 
-// the same, after this wave's LDS reads have returned too (the pipelined loop reads a stage ahead of its MFMAs)
-template <int N>
-__device__ inline void chunk_barrier_lgkm() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
 // 8 fp32 -> hi / lo fp16 fragments (RNE twice)
 __device__ inline void split8(const float4& p, const float4& q, half8_t& hi, half8_t& lo) {
   const float x[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
@@ -129,7 +122,7 @@ extern "C" int dd_x5_stamps_read(unsigned long long* h, int n) {
 
 // PREC 0: f16x3; PREC 1: the bf16 mode (A converted to bf16 at fragment-read time, B = the bf16 weight
 // image, one v_mfma_f32_32x32x16_bf16 per MAC; the stage's second B image is not filled).
-template <int WM, int WN, int TM, int TN, int MODE, int NS, int PREC, int PIPE>
+template <int WM, int WN, int TM, int TN, int MODE, int NS, int PREC>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 (scalar tap walk, per-row tap masks); MODE 0: generic K.
@@ -294,70 +287,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   for (int u = 0; u < NS - 1; ++u) issue(u, u * KC);
   int cur = 0;  // stage of chunk kc
   X5_STAMP(1);
-  if constexpr (PIPE && PREC == 0) {
-    // Software-pipelined chunk walk: [reads (kc, k16 half 1)] [MFMAs (kc, half 0)] [barrier: chunk kc+1 landed,
-    // every wave's reads of chunk kc returned] [DMA chunk kc+NS into kc's stage] [reads (kc+1, half 0)]
-    // [MFMAs (kc, half 1)]: every fragment read is in flight under the previous half's MFMAs. A is kept as
-    // fp32 in the fragment registers and split right before its MFMAs (a split beside the reads would wait
-    // for them).
-    struct Frag {
-      float4 ap[TM][2];
-      half8_t bh[TN], bl[TN];
-    };
-    auto read_frag = [&](Frag& F, const char* st, auto S2) {
-      constexpr int s2 = decltype(S2)::value;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        F.bh[j] = *reinterpret_cast<const half8_t*>(st + b_ro[s2][j]);
-        F.bl[j] = *reinterpret_cast<const half8_t*>(st + b_ro[s2][j] + BB);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        F.ap[i][0] = *reinterpret_cast<const float4*>(st + a_ro[s2][i][0]);
-        F.ap[i][1] = *reinterpret_cast<const float4*>(st + a_ro[s2][i][1]);
-      }
-    };
-    auto mfma_frag = [&](const Frag& F) {
-      half8_t ah[TM], al[TM];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) split8(F.ap[i][0], F.ap[i][1], ah[i], al[i]);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], F.bh[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], F.bl[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], F.bh[j], acc[i][j], 0, 0, 0);
-    };
-    using H0 = std::integral_constant<int, 0>;
-    using H1 = std::integral_constant<int, 1>;
-    Frag F0, F1;
-    chunk_barrier<(NS - 2) * DPC>();  // chunk 0 landed
-    issue(NS - 1, (NS - 1) * KC);
-    read_frag(F0, lds, H0());
-    for (int kc = 0; kc < nk; ++kc) {
-      read_frag(F1, lds + cur * STAGE, H1());
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_frag(F0);
-      __builtin_amdgcn_sched_barrier(0);
-      chunk_barrier_lgkm<(NS - 2) * DPC>();
-      issue(cur, (kc + NS) * KC);
-      if (++cur == NS) cur = 0;
-      read_frag(F0, lds + cur * STAGE, H0());  // past the last chunk: the all-OOB (zero) stage, unused
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_frag(F1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    chunk_barrier_lgkm<0>();  // drain the trailing DMAs and reads before the epilogue reuses the LDS
-  } else {
   for (int kc = 0; kc < nk; ++kc) {
     // this wave's DMAs of chunk kc have landed (NS-2 younger chunks may fly), every wave's have
     // (barrier), and every wave finished reading chunk kc-1, whose stage is refilled below
@@ -417,7 +346,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
     }
   }
   chunk_barrier<0>();  // drain the trailing (all-OOB) DMAs before the block retires
-  }
   X5_STAMP(2);
 
   // ---- epilogue: 16-B quads through LDS when every row is 16-B aligned, else per accumulator element
@@ -484,12 +412,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
 #endif
 }
 
-// DDMI_X5_PIPE (read per dispatch, micro-benchmark A/B): 1 = the software-pipelined chunk walk for f16x3
-static bool x5_pipe() {
-  const char* e = getenv("DDMI_X5_PIPE");
-  return e && atoi(e) != 0;
-}
-
 template <int WM, int WN, int TM, int TN, int NS, int PREC>
 static void launch_x5_one(const ConvArgs& a, int M, int K, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -499,21 +421,12 @@ static void launch_x5_one(const ConvArgs& a, int M, int K, hipStream_t st) {
   static const std::string name =
       "conv_x5<" + std::to_string(BM) + "," + std::to_string(BN) + (PREC ? ",bf16>" : ">");
   set_last_conv_config(name.c_str());
-  const bool m1 = a.Cin % KC == 0 && a.KH * a.KW <= 32;
-  if (PREC == 0 && x5_pipe()) {
-    if (m1)
-      hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS, PREC, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K,
-                         ntm, ntn);
-    else
-      hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS, PREC, 1>), grid, dim3(64 * WM * WN), 0, st, a, M, K,
-                         ntm, ntn);
-  } else if (m1) {
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS, PREC, 0>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
+  if (a.Cin % KC == 0 && a.KH * a.KW <= 32)
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS, PREC>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
                        ntn);
-  } else {
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS, PREC, 0>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
+  else
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS, PREC>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
                        ntn);
-  }
   DD_HIP_CHECK(hipGetLastError());
 }
 template <int WM, int WN, int TM, int TN, int NS>

@@ -1,12 +1,10 @@
 #!/bin/bash
-# Round-4 (e): the training-head GPU tests, the conv_x5 pipelined-walk A/B (tools/gpu_x5pipe.sh); then the handle-lifetime investigation: the minimal reproducer with every
 # stream of the process re-created per iteration, and the round-3 reproducing order with the dbg library and the pool
 # off (a segfault in either is the finding: nothing runs after it).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_train_loss.py -v -m gpu -x --timeout 200 --timeout-method thread \
   > gpurun_out/train_tests.log 2>&1; rc=$?; tail -3 gpurun_out/train_tests.log; [ $rc -ne 0 ] && exit $rc
-bash tools/gpu_x5pipe.sh || exit $?
 timeout -k 10 200 tools/repro/graph_churn 150 0 64 1 > gpurun_out/churn_all.log 2>&1; rc=$?
 echo "[churn_all] rc=$rc"; tail -2 gpurun_out/churn_all.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 env DDMI_STREAM_POOL=0 DDMI_LIB=$R/diffusiondrive_amd/_variants/libddmi_dbg.so python -u -m pytest \
