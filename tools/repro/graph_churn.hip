@@ -4,12 +4,14 @@
 // hand-off from the caller's stream, or single-stream directly on a long-lived caller stream), replayed, then the
 // handle torn down in runtime.cpp ~Model's order (sync, exec destroy, events, streams, buffer).
 //
-//   graph_churn <iterations> <pool 0|1> <kernels per branch> [all 0|1]
+//   graph_churn <iterations> <pool 0|1> <kernels per branch> [all 0|1] [forks] [memset 0|1]
 //
 // pool 1 keeps destroyed handles' streams for the next handles (runtime.cpp's process-wide pool), pool 0 destroys
 // them. all 1: no stream outlives an iteration (the caller streams and the long-lived handle are re-created every
 // iteration too), so the runtime's hardware queues - GPU_MAX_HW_QUEUES, shared round-robin by streams - can be
-// released and re-created between handles. Prints one line per 25 iterations; a segfault ends the process (the
+// released and re-created between handles. forks: fork / join pairs to the side stream per captured body (the
+// forward's LiDAR-trunk, time-MLP, tf-decoder and heads branches all fork to one side stream); memset 1: a
+// hipMemsetAsync node on each branch. Prints one line per 25 iterations; a segfault ends the process (the
 // driving script reports the exit code).
 #include <hip/hip_runtime.h>
 
@@ -32,6 +34,8 @@ __global__ void k_add(float* p, int n, float v) {
 }
 
 static bool g_pool = true;
+static int g_forks = 1;
+static bool g_memset = false;
 static std::vector<hipStream_t> g_streams;
 
 static hipStream_t take_stream() {
@@ -53,7 +57,8 @@ static void give_stream(hipStream_t s) {
 
 struct Handle {
   hipStream_t s_main = nullptr, s_side = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr, fj[2] = {nullptr, nullptr};
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  std::vector<hipEvent_t> fj;
   hipGraphExec_t ex = nullptr;
   float* buf = nullptr;
   int n = 1 << 16, K = 64, calls = 0;
@@ -64,6 +69,7 @@ struct Handle {
     s_side = take_stream();
     CK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+    fj.resize(2 * g_forks);
     for (auto& e : fj) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     CK(hipMalloc(&buf, 2 * n * sizeof(float)));
     CK(hipMemsetAsync(buf, 0, 2 * n * sizeof(float), s_main));
@@ -75,14 +81,20 @@ struct Handle {
       for (int k = 0; k < 2 * K; ++k) hipLaunchKernelGGL(k_add, g, b, 0, st, buf + (k & 1) * n, n, 1.0f);
       return;
     }
-    CK(hipEventRecord(fj[0], st));
-    CK(hipStreamWaitEvent(s_side, fj[0], 0));
-    for (int k = 0; k < K; ++k) {
-      hipLaunchKernelGGL(k_add, g, b, 0, st, buf, n, 1.0f);
-      hipLaunchKernelGGL(k_add, g, b, 0, s_side, buf + n, n, 2.0f);
+    for (int f = 0; f < g_forks; ++f) {
+      CK(hipEventRecord(fj[2 * f], st));
+      CK(hipStreamWaitEvent(s_side, fj[2 * f], 0));
+      if (g_memset) {
+        CK(hipMemsetAsync(buf + n, 0, 1024, s_side));
+        CK(hipMemsetAsync(buf, 0, 1024, st));
+      }
+      for (int k = 0; k < K / g_forks; ++k) {
+        hipLaunchKernelGGL(k_add, g, b, 0, st, buf, n, 1.0f);
+        hipLaunchKernelGGL(k_add, g, b, 0, s_side, buf + n, n, 2.0f);
+      }
+      CK(hipEventRecord(fj[2 * f + 1], s_side));
+      CK(hipStreamWaitEvent(st, fj[2 * f + 1], 0));
     }
-    CK(hipEventRecord(fj[1], s_side));
-    CK(hipStreamWaitEvent(st, fj[1], 0));
   }
   void forward(hipStream_t caller) {
     const bool direct = single && caller != nullptr;
@@ -126,6 +138,12 @@ int main(int argc, char** argv) {
   g_pool = argc > 2 ? atoi(argv[2]) != 0 : true;
   const int K = argc > 3 ? atoi(argv[3]) : 64;
   const bool all = argc > 4 && atoi(argv[4]) != 0;
+  g_forks = argc > 5 ? atoi(argv[5]) : 1;
+  g_memset = argc > 6 && atoi(argv[6]) != 0;
+  if (g_forks < 1 || g_forks > K) {
+    std::fprintf(stderr, "forks must be in [1, kernels per branch]\n");
+    return 2;
+  }
   CK(hipSetDevice(0));
   hipStream_t callers[3];
   for (auto& s : callers) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));  // torch's pooled streams
@@ -160,7 +178,7 @@ int main(int argc, char** argv) {
   }
   delete keep;
   for (auto& s : callers) CK(hipStreamDestroy(s));
-  std::printf("graph_churn: %d iterations, pool %d, %d kernels per branch, all %d: no fault\n", iters, (int)g_pool, K,
-              (int)all);
+  std::printf("graph_churn: %d iterations, pool %d, %d kernels per branch, all %d, forks %d, memset %d: no fault\n", iters,
+              (int)g_pool, K, (int)all, g_forks, (int)g_memset);
   return 0;
 }
