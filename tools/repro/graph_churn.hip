@@ -176,7 +176,15 @@ int main(int argc, char** argv) {
       std::fflush(stdout);
     }
   }
+  // the long-lived handle destroyed, then a fresh two-stream handle (which takes its streams' recycled objects):
+  // eager, captured (instantiate + first launch), replayed - the shape of the faulting test order
   delete keep;
+  {
+    Handle e(false, K);
+    for (int r = 0; r < 3; ++r) e.forward(nullptr);
+    CK(hipDeviceSynchronize());
+  }
+  std::printf("final fresh handle after the long-lived one: ok\n");
   for (auto& s : callers) CK(hipStreamDestroy(s));
   std::printf("graph_churn: %d iterations, pool %d, %d kernels per branch, all %d, forks %d, memset %d: no fault\n", iters,
               (int)g_pool, K, (int)all, g_forks, (int)g_memset);
