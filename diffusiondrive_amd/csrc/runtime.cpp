@@ -191,7 +191,11 @@ class Model {
   // fork / join events of one forward (reused across forwards: every record precedes its wait)
   std::vector<hipEvent_t> fj_ev;
   size_t fj_next = 0;
-  bool use_side = true;  // DDMI_STREAMS=0: everything on the main stream
+  // Single-stream graphs by default. Two-stream graphs (DDMI_STREAMS=1 or dd_set_streams(h, 2)) are opt-in: the HIP
+  // runtime's graph launch (ROCm 7.2) reads past its candidate-stream list when the exec's internal branch streams
+  // share the launch stream's hardware queue, a host segfault that depends on the process's queue history (DESIGN.md
+  // section 4, Handle lifetime). Batches-in-flight lanes were single-stream already.
+  bool use_side = false;
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
   bool value_dedup = true;
@@ -233,6 +237,10 @@ class Model {
   // graph cache keyed by the forward's shape signature; every entry belongs to the current buffer
   // generation (the cache is emptied when a workspace buffer is (re)allocated: graphs hold its pointers)
   std::map<std::string, hipGraphExec_t> graphs;
+  void drop_graphs() {
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
+    graphs.clear();
+  }
   uint64_t graph_gen = 0;
   uint64_t generation = 0;  // bumped whenever a workspace buffer is (re)allocated
   std::set<std::string> known_shapes;
@@ -356,7 +364,7 @@ class Model {
     if (ev_out) (void)hipEventSynchronize(ev_out);  // the last forward, also when it ran on a caller's stream
     if (st_main) (void)hipStreamSynchronize(st_main);
     if (st_side) (void)hipStreamSynchronize(st_side);
-    for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
+    drop_graphs();
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     for (auto& e : fj_ev) (void)hipEventDestroy(e);
@@ -1969,8 +1977,7 @@ class Model {
       if (graph_gen != generation || graphs.size() > 8) {
         // an earlier replay may still run (on the caller's stream in direct mode): ev_out marks the last forward
         DD_HIP_CHECK(hipEventSynchronize(ev_out));
-        for (auto& g : graphs) DD_HIP_CHECK(hipGraphExecDestroy(g.second));
-        graphs.clear();
+        drop_graphs();
         graph_gen = generation;
       }
       auto it = graphs.find(key);
@@ -2185,8 +2192,7 @@ int dd_set_streams(dd_handle* h, int n) {
     if (m.use_side == (n == 2)) return;
     DD_HIP_CHECK(hipStreamSynchronize(m.st));
     DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a graph replayed on a caller's stream may still run
-    for (auto& g : m.graphs) DD_HIP_CHECK(hipGraphExecDestroy(g.second));  // captured with the other topology
-    m.graphs.clear();
+    m.drop_graphs();  // captured with the other topology
     m.use_side = n == 2;
   });
 }

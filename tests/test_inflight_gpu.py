@@ -18,38 +18,44 @@ def _inputs(B, seed):
     return {k: torch.from_numpy(inp[k]).to(DEV) for k in KEYS}, torch.from_numpy(inp["noise"]).to(DEV)
 
 
-def test_single_stream_forward_matches_two_stream(gpu_model):
-    """dd_set_streams(1) (one stream; on a non-default caller stream the graph replays on that stream) against the
-    default two-stream graph on the same batch: the same kernels in another order - equal up to the value_proj split
-    choice, which depends on the CUs the concurrent tf-decoder branch holds (1.5e-6 class)."""
+def test_caller_stream_replay_matches_own_stream(gpu_model):
+    """A single-stream handle (the default) called on a non-default caller stream replays its graph on that stream
+    (no hand-off); called on the default stream it runs on its own stream behind an event hand-off. Same kernels in
+    the same order: bit-identical."""
     feats, noise = _inputs(4, 7)
-    ref = gpu_model.forward(feats, noise=noise)["trajectory"].cpu()
     m = gpu_model
-    try:
-        m.set_streams(1)
-        s = torch.cuda.Stream(DEV)
-        s.wait_stream(torch.cuda.current_stream())
-        for _ in range(2):  # eager (first call of the shape), then the captured graph on the caller's stream
-            with torch.cuda.stream(s):
-                out = m.forward(feats, noise=noise, stream=s)["trajectory"]
-            s.synchronize()
-            assert float((out.cpu() - ref).abs().max()) <= 1e-5
-        # the flag / tap readers wait for a forward that ran on the caller's stream
-        assert m.numerics_flags() == 0
-        assert m.tap("trajectory").numel() >= 4 * 8 * 3
-        # the default (null) stream keeps the hand-off through the handle's own stream
-        out0 = m.forward(feats, noise=noise)["trajectory"].cpu()
-        assert torch.equal(out0, out.cpu())
-    finally:
-        m.set_streams(2)
-    assert torch.equal(gpu_model.forward(feats, noise=noise)["trajectory"].cpu(), ref)
+    assert m.stream_count() == 1
+    ref = m.forward(feats, noise=noise)["trajectory"].cpu()
+    s = torch.cuda.Stream(DEV)
+    s.wait_stream(torch.cuda.current_stream())
+    for _ in range(2):  # eager (first call of the shape), then the captured graph on the caller's stream
+        with torch.cuda.stream(s):
+            out = m.forward(feats, noise=noise, stream=s)["trajectory"]
+        s.synchronize()
+        assert torch.equal(out.cpu(), ref)
+    # the flag / tap readers wait for a forward that ran on the caller's stream
+    assert m.numerics_flags() == 0
+    assert m.tap("trajectory").numel() >= 4 * 8 * 3
+    assert torch.equal(m.forward(feats, noise=noise)["trajectory"].cpu(), ref)
+
+
+def test_two_stream_graphs_in_a_fresh_process():
+    """The opt-in two-stream graphs (dd_set_streams(h, 2)) in a child process of their own: against the single-stream
+    graph (within 1e-5: the same kernels, another order), and after 16 clones in both modes came and went. A fresh
+    process because the HIP runtime's multi-stream graph launch faults with a history-dependent hardware-queue
+    assignment (Handle lifetime); a fault here fails this test, not the suite."""
+    import os
+    import subprocess
+    import sys
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "two_stream_child.py")
+    r = subprocess.run([sys.executable, child], capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0 and "two_stream_child: ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
 
 
 @pytest.mark.parametrize("lanes", [2, 3])
 def test_inflight_planner_matches_one_at_a_time(seeded_sd, lanes):
     """2 x lanes forwards of different batches queued back to back over the lanes, read after one synchronize:
-    every result bit-equal to the same batch run alone on a single-stream handle (the lanes are such handles), and
-    within 1e-5 of the default two-stream forward."""
+    every result bit-equal to the same batch run alone on a single-stream handle (the lanes are such handles)."""
     pl = InFlightPlanner(state_dict=seeded_sd, device=0, lanes=lanes)
     solo = DiffusionDriveModel(state_dict=seeded_sd, device=0)
     try:
@@ -57,12 +63,9 @@ def test_inflight_planner_matches_one_at_a_time(seeded_sd, lanes):
         outs = [pl.forward(f, noise=nz)["trajectory"] for f, nz in batches]
         pl.synchronize()
         assert pl.numerics_flags() == 0
-        ref2 = [solo.forward(f, noise=nz)["trajectory"].cpu() for f, nz in batches]
-        solo.set_streams(1)
         ref1 = [solo.forward(f, noise=nz)["trajectory"].cpu() for f, nz in batches]
         for i, o in enumerate(outs):
             assert torch.equal(o.cpu(), ref1[i]), f"batch {i} (lane {i % lanes})"
-            assert float((o.cpu() - ref2[i]).abs().max()) <= 1e-5
         # distinct batches gave distinct trajectories (no lane read another lane's buffers)
         assert len({float(o.sum()) for o in outs}) == len(outs)
     finally:
@@ -143,11 +146,10 @@ def test_inflight_inputs_dropped_right_after_forward(seeded_sd):
         solo.close()
 
 
-def test_handle_churn_then_two_stream_replay(seeded_sd):
-    """Regression for the round-3 host segfault inside hipGraphLaunch after many handles were created and destroyed
-    (DESIGN.md section 4, Handle lifetime): 32 clones are created, run in both stream modes (eager, captured, replayed;
-    single-stream ones on caller streams) and destroyed, then the first handle's two-stream graph is replayed and
-    must give its earlier result bit for bit."""
+def test_handle_churn_then_replay(seeded_sd):
+    """Handle churn (DESIGN.md section 4, Handle lifetime): 32 clones are created, run (eager, captured, replayed;
+    every other one on a caller stream, the rest on their own streams) and destroyed, then the first handle's graph is
+    replayed and must give its earlier result bit for bit."""
     base = DiffusionDriveModel(state_dict=seeded_sd, device=0)
     try:
         f, nz = _inputs(1, 41)
@@ -156,9 +158,7 @@ def test_handle_churn_then_two_stream_replay(seeded_sd):
         for i in range(32):
             c = base.clone()
             try:
-                single = i % 2 == 1
-                c.set_streams(1 if single else 2)
-                s = streams[i % 3] if single else None
+                s = streams[i % 3] if i % 2 else None
                 for _ in range(3):
                     if s is not None:
                         s.wait_stream(torch.cuda.current_stream())
@@ -167,7 +167,7 @@ def test_handle_churn_then_two_stream_replay(seeded_sd):
                         s.synchronize()
                     else:
                         out = c.forward(f, noise=nz)["trajectory"]
-                assert float((out.cpu() - ref).abs().max()) <= 1e-5, i
+                assert torch.equal(out.cpu(), ref), i
             finally:
                 c.close()
         for _ in range(3):
