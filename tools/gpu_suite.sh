@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 (o): single-stream graphs by default. (1) the reproducing order with the stream pool off (the worst history
+# The round-end GPU checks: (1) the reproducing order with the stream pool off (the worst history
 # seen); (2) the whole GPU suite in its default order (the driver's round-end run); (3) smoke(). Stops at a failure.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
