@@ -15,6 +15,7 @@ All inputs synthetic and seeded, weights seeded random (no checkpoint download),
 in HBM, hipGraph replay, device-synchronised wall clock over `steps` forwards after warmup.
 """
 import argparse
+import subprocess
 import json
 import os
 import sys
@@ -82,6 +83,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "configs"))
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--c1-two-stream", action="store_true",
+                    help="child mode: C1 batch-1 latency with the opt-in two-stream graph, one JSON line")
     a = ap.parse_args()
     from diffusiondrive_amd.config import TransfuserConfig
     from diffusiondrive_amd.model import DiffusionDriveModel
@@ -100,6 +103,18 @@ def main():
         ctx.update(cfg=cfg, sd=sd, inp=inp)
         feats = {k: torch.from_numpy(inp[k]).to(dev) for k in ("camera_feature", "lidar_feature", "status_feature")}
         return m, feats, torch.from_numpy(inp["noise"]).to(dev)
+
+    if a.c1_two_stream:  # a fresh process of its own (Handle lifetime)
+        m, feats, noise = setup("resnet34", 1)
+        m.set_streams(2)
+        rows = {}
+        for mode in ("f16x3", "bf16", "fp32"):
+            m.set_gemm_mode(mode)
+            ms, _ = timed(m, feats, noise, 2, 5 * a.steps)
+            rows[mode] = {"ms_per_batch": round(ms, 3), "scenes_per_s": round(1 / ms * 1e3, 2)}
+        m.close()
+        print("C1TWO " + json.dumps(rows), flush=True)
+        return
 
     # ---- C1 / C2 (ResNet-34)
     for B, key in ((1, "C1_batch1_latency"), (64, "C2_batch64")):
@@ -251,6 +266,21 @@ def main():
                   "batch 64, f16x3:", "", "| path | ms / batch | scenes/s |", "|---|---|---|"]
     for k, v in e2e_rows.items():
         lines.append(f"| {k} | {v['ms_per_batch']} | {v['scenes_per_s']} |")
+    # C1 with the opt-in two-stream graph, in a child process (a runtime fault there loses only this table)
+    r2 = subprocess.run([sys.executable, os.path.abspath(__file__), "--c1-two-stream", "--steps", str(a.steps)],
+                        capture_output=True, text=True, timeout=600)
+    two = [ln for ln in r2.stdout.splitlines() if ln.startswith("C1TWO ")]
+    lines += ["", "C1 batch-1 latency with the opt-in two-stream graph (dd_set_streams(h, 2); fresh process):", "",
+              "| gemm | ms / batch | scenes/s |", "|---|---|---|"]
+    if r2.returncode == 0 and two:
+        rows2 = json.loads(two[-1][6:])
+        res["configs"]["C1_batch1_latency_two_stream"] = {"arch": "resnet34", "batch": 1, "ddim_steps": 2,
+                                                          "streams": 2, "modes": rows2}
+        lines += [f"| {k} | {v['ms_per_batch']} | {v['scenes_per_s']} |" for k, v in rows2.items()]
+    else:
+        lines.append(f"| (child exited {r2.returncode}) | - | - |")
+    with open(a.out + ".json", "w") as f:
+        json.dump(res, f, indent=1)
     with open(a.out + ".md", "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
