@@ -119,7 +119,7 @@ static void trunk_channels(int arch, int ch[5], bool& bottleneck) {
 // handle's two-stream graph (ROCm 7.2; reproduced by tests/test_runner.py + test_inflight_gpu.py + test_agent.py in
 // that order, the fault inside libamdhip64 under hipGraphLaunch).
 static std::mutex g_stream_pool_mu;
-static std::map<int, std::vector<hipStream_t>> g_stream_pool;
+static std::map<std::pair<int, int>, std::vector<hipStream_t>> g_stream_pool;  // (device, priority)
 
 static bool stream_pool_on() {
   static const bool on = [] {
@@ -129,10 +129,10 @@ static bool stream_pool_on() {
   return on;
 }
 
-static hipStream_t pooled_stream(int device) {
+static hipStream_t pooled_stream(int device, int priority = 0) {
   if (stream_pool_on()) {
     std::lock_guard<std::mutex> lk(g_stream_pool_mu);
-    auto& v = g_stream_pool[device];
+    auto& v = g_stream_pool[{device, priority}];
     if (!v.empty()) {
       hipStream_t s = v.back();
       v.pop_back();
@@ -140,18 +140,18 @@ static hipStream_t pooled_stream(int device) {
     }
   }
   hipStream_t s = nullptr;
-  DD_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  DD_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
   return s;
 }
 
-static void release_stream(int device, hipStream_t s) {
+static void release_stream(int device, hipStream_t s, int priority = 0) {
   (void)hipStreamSynchronize(s);
   if (!stream_pool_on()) {
     (void)hipStreamDestroy(s);
     return;
   }
   std::lock_guard<std::mutex> lk(g_stream_pool_mu);
-  g_stream_pool[device].push_back(s);
+  g_stream_pool[{device, priority}].push_back(s);
 }
 
 class Model {
@@ -196,6 +196,7 @@ class Model {
   // share the launch stream's hardware queue, a host segfault that depends on the process's queue history (DESIGN.md
   // section 4, Handle lifetime). Batches-in-flight lanes were single-stream already.
   bool use_side = false;
+  int main_prio = 0;  // priority of st_main (DDMI_MAIN_PRIORITY)
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
   bool value_dedup = true;
@@ -290,7 +291,16 @@ class Model {
     }
     // default-priority streams: either one at the device's greatest priority measured 3-3.5 % slower
     // in the B = 64 bench graph, both at the least priority 33 % slower
-    st_main = pooled_stream(device);
+    // DDMI_MAIN_PRIORITY=1 (experiment): the handle's own (launch) stream at the device's greatest priority, whose
+    // hardware queues are a separate pool from the normal-priority ones the runtime gives a multi-stream exec's
+    // branch streams (Handle lifetime)
+    if (const char* e = getenv("DDMI_MAIN_PRIORITY"))
+      if (atoi(e) != 0) {
+        int least = 0, greatest = 0;
+        DD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        main_prio = greatest;
+      }
+    st_main = pooled_stream(device, main_prio);
     st_side = pooled_stream(device);
     st = st_own = st_main;
     DD_TRACE("create model %p st_main=%p st_side=%p", (void*)this, (void*)st_main, (void*)st_side);
@@ -368,7 +378,7 @@ class Model {
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     for (auto& e : fj_ev) (void)hipEventDestroy(e);
-    if (st_main) release_stream(device, st_main);
+    if (st_main) release_stream(device, st_main, main_prio);
     if (st_side) release_stream(device, st_side);
     if (num_flags) (void)hipFree(num_flags);
     if (in_tab) (void)hipFree(in_tab);

@@ -24,19 +24,23 @@ def test_caller_stream_replay_matches_own_stream(gpu_model):
     the same order: bit-identical."""
     feats, noise = _inputs(4, 7)
     m = gpu_model
-    assert m.stream_count() == 1
-    ref = m.forward(feats, noise=noise)["trajectory"].cpu()
-    s = torch.cuda.Stream(DEV)
-    s.wait_stream(torch.cuda.current_stream())
-    for _ in range(2):  # eager (first call of the shape), then the captured graph on the caller's stream
-        with torch.cuda.stream(s):
-            out = m.forward(feats, noise=noise, stream=s)["trajectory"]
-        s.synchronize()
-        assert torch.equal(out.cpu(), ref)
-    # the flag / tap readers wait for a forward that ran on the caller's stream
-    assert m.numerics_flags() == 0
-    assert m.tap("trajectory").numel() >= 4 * 8 * 3
-    assert torch.equal(m.forward(feats, noise=noise)["trajectory"].cpu(), ref)
+    n0 = m.stream_count()
+    try:
+        m.set_streams(1)
+        ref = m.forward(feats, noise=noise)["trajectory"].cpu()
+        s = torch.cuda.Stream(DEV)
+        s.wait_stream(torch.cuda.current_stream())
+        for _ in range(2):  # eager (first call of the shape), then the captured graph on the caller's stream
+            with torch.cuda.stream(s):
+                out = m.forward(feats, noise=noise, stream=s)["trajectory"]
+            s.synchronize()
+            assert torch.equal(out.cpu(), ref)
+        # the flag / tap readers wait for a forward that ran on the caller's stream
+        assert m.numerics_flags() == 0
+        assert m.tap("trajectory").numel() >= 4 * 8 * 3
+        assert torch.equal(m.forward(feats, noise=noise)["trajectory"].cpu(), ref)
+    finally:
+        m.set_streams(n0)
 
 
 def test_two_stream_graphs_in_a_fresh_process():
