@@ -18,6 +18,7 @@ def main():
     feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
     nz = torch.from_numpy(inp["noise"]).cuda()
     one = DiffusionDriveModel(cfg, seeded_state_dict(cfg, 0), device=0, gemm="f16x3")
+    one.set_streams(1)  # explicit: the environment may set the default ($DDMI_STREAMS)
     two = one.clone()
     two.set_streams(2)
     assert one.stream_count() == 1 and two.stream_count() == 2
