@@ -28,7 +28,6 @@
 //    loaded into registers while the current tile's MFMAs run.
 // Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.17 x recompute,
 // 224 / 196 K padding; HBM traffic = the input once (+ halo re-reads) + the pooled map.
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -72,12 +71,6 @@ constexpr int MSTEP = NT / 128;                    // M-tile stride of a wave (w
 constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread per tile
 constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
 constexpr int LDS_BYTES = 2 * IMG_BYTES + NMT * 32 * SOP * 4;
-// One input channel (the LiDAR histogram, SRC_C = 1): K = 7 kh x 8 kw = 56 -> 4 k16 steps instead of 14 (the
-// 4-channel layout's three zero channels dropped); a lane's fragment is 8 consecutive input pixels of one kernel row
-// (kw 0..7, kw 7 a zero weight), read as four 4-B words from a [IH][IP1] fp16 patch; the zero kernel row kh = 7 reads
-// row 6 (finite values times zero weights).
-constexpr int KS1 = 4;
-constexpr int IP1 = 40;                            // 1-channel patch pitch (halfs): even -> 4-B aligned fragments
 
 __device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
   hi = __builtin_convertvector(v, sp_h4);
@@ -106,30 +99,8 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
   const int nt = wave & 1, mg = wave >> 1;
   const int co = nt * 32 + li;
 
-  constexpr bool ONE = SRC_C == 1;
-  constexpr int NCH = SRC_C == 4 ? 1 : SRC_C;  // SRC_C = 4: one NCHW channel through the 4-channel layout (A/B)
-  constexpr int KSX = ONE ? KS1 : KS;
-  // ---- loop-invariant B fragments of this wave's 32 channels (k = kh*28 + kw*4 + ci; one channel: k = kh*8 + kw)
-  sp_h8 bh[KSX], bl[KSX];
-  if constexpr (ONE) {
-#pragma unroll
-    for (int s = 0; s < KS1; ++s) {
-      const int kh = 2 * s + hl;
-      uint16_t hv[8], lv[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bool w = kh < 7 && e < 7;
-        const int64_t o = (int64_t)co * ldh + kh * 28 + e * 4;
-        hv[e] = w ? wh[o] : (uint16_t)0;
-        lv[e] = (w && !PREC) ? wl[o] : (uint16_t)0;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        bh[s][e] = __builtin_bit_cast(_Float16, hv[e]);
-        bl[s][e] = __builtin_bit_cast(_Float16, lv[e]);
-      }
-    }
-  } else
+  // ---- loop-invariant B fragments of this wave's 32 channels (k = kh*28 + kw*4 + ci)
+  sp_h8 bh[KS], bl[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int kh = s >> 1, kw0 = 4 * (s & 1) + 2 * hl;
@@ -173,12 +144,12 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
                     : (sp_f4){0.f, 0.f, 0.f, 0.f};
       } else {
         // consecutive threads take consecutive columns: each plane's loads coalesce
-        const float* p = img + (int64_t)b * NCH * plane + (int64_t)iy * W + ix;
+        const float* p = img + (int64_t)b * SRC_C * plane + (int64_t)iy * W + ix;
         sp_f4 v = {0.f, 0.f, 0.f, 0.f};
         if (ok) {
           v.x = p[0];
-          if constexpr (NCH > 1) v.y = p[plane];
-          if constexpr (NCH > 2) v.z = p[2 * plane];
+          if constexpr (SRC_C > 1) v.y = p[plane];
+          if constexpr (SRC_C > 2) v.z = p[2 * plane];
         }
         pre[i] = v;
       }
@@ -190,16 +161,6 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       const int e = tid + NT * i;
       if (e < IH * IW) {
         const int r = e / IW, c = e - (e / IW) * IW;
-        if constexpr (ONE) {
-          if constexpr (PREC == 1) {
-            reinterpret_cast<__bf16*>(in_hi)[r * IP1 + c] = (__bf16)pre[i].x;
-          } else {
-            const _Float16 h = (_Float16)pre[i].x;
-            reinterpret_cast<_Float16*>(in_hi)[r * IP1 + c] = h;
-            reinterpret_cast<_Float16*>(in_lo)[r * IP1 + c] = (_Float16)(pre[i].x - (float)h);
-          }
-          continue;
-        }
         if constexpr (PREC == 1) {
           *reinterpret_cast<sp_b4*>(in_hi + (r * IP + c) * 8) = __builtin_convertvector(pre[i], sp_b4);
         } else {
@@ -230,28 +191,6 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       sp_f16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      if constexpr (ONE) {
-        const int base1 = (2 * ly) * IP1 + 2 * lx;  // halfs: input pixel of (kh 0, kw 0)
-        auto frag = [&](const char* img, int kh) {
-          const uint32_t* w = reinterpret_cast<const uint32_t*>(img) + ((base1 + kh * IP1) >> 1);
-          const uint4 u = make_uint4(w[0], w[1], w[2], w[3]);
-          return __builtin_bit_cast(sp_h8, u);
-        };
-#pragma unroll
-        for (int s = 0; s < KS1; ++s) {
-          const int kh = min(2 * s + hl, 6);
-          const sp_h8 ah = frag(in_hi, kh);
-          if constexpr (PREC == 1) {
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_b8, ah),
-                                                          __builtin_bit_cast(sp_b8, bh[s]), acc, 0, 0, 0);
-          } else {
-            const sp_h8 al = frag(in_lo, kh);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
-          }
-        }
-      } else
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int off = (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
@@ -309,13 +248,6 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
 
 }  // namespace
 
-// DDMI_STEM1=0 (read per dispatch: graph capture; A/B): a one-channel NCHW input through the 4-channel layout (K = 224)
-// instead of the one-channel K = 64 form
-static bool stem1_on() {
-  const char* e = getenv("DDMI_STEM1");
-  return !(e && atoi(e) == 0);
-}
-
 // Returns false when the conv is not a 7x7 / s2 / p3, Cin 4, Cout 64 f16x3 / bf16 stem on a contiguous
 // NHWC4 input (src == nullptr) or on the NCHW tensor of src_c channels whose address is the device word *src
 // (the caller then runs the conv and the pool separately).
@@ -345,7 +277,7 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int per_cu = NT == 512 ? 1 : 2;
   const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
-  static std::atomic<uint64_t> attr[2][5];
+  static std::atomic<uint64_t> attr[2][4];
   auto go = [&](auto kern, int c) {
     set_max_lds_once(attr[a.prec][c], reinterpret_cast<const void*>(kern), LDS_BYTES);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, src, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
@@ -355,9 +287,7 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   auto pick = [&](auto PR) {
     constexpr int P = decltype(PR)::value;
     switch (c) {
-      case 1:
-        if (stem1_on()) go(stem_pool_kernel<P, 1>, 1); else go(stem_pool_kernel<P, 4>, 4);
-        break;
+      case 1: go(stem_pool_kernel<P, 1>, 1); break;
       case 2: go(stem_pool_kernel<P, 2>, 2); break;
       case 3: go(stem_pool_kernel<P, 3>, 3); break;
       default: go(stem_pool_kernel<P, 0>, 0); break;

@@ -501,10 +501,9 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
 @pytest.mark.parametrize("mode", ["f16x3", "bf16"])
 def test_nchw_stem_equals_nhwc4_stem(gpu_model, seeded_sd, monkeypatch, mode):
     """The fused stems read the caller's NCHW camera / LiDAR tensors in place (through the handle's device input
-    table) instead of an NHWC4 copy made by a transpose pass first (DDMI_STEM_NCHW=0): the camera's 4-channel pixels
-    reach the same arithmetic (bit-identical pooled map), the one-channel LiDAR input its K = 64 form (within
-    accumulation rounding); a forward whose inputs sit at new addresses gives the same trajectory bit for bit (the
-    captured graph reads the table, not a baked pointer)."""
+    table) instead of an NHWC4 copy made by a transpose pass first (DDMI_STEM_NCHW=0): the same 4-channel pixels
+    reach the same arithmetic, so the pooled stem maps and the trajectory are bit-identical - also on a forward
+    whose inputs sit at new addresses (the captured graph reads the table, not a baked pointer)."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
     B = 3
@@ -525,12 +524,6 @@ def test_nchw_stem_equals_nhwc4_stem(gpu_model, seeded_sd, monkeypatch, mode):
     ref = m.forward(feats, noise=nz)["trajectory"].cpu().numpy()
     ref_pools = [m.tap(n).cpu().numpy() for n in ("img_pool", "lid_pool")]
     m.close()
-    # the camera stem runs the same arithmetic either way: bit-identical. The one-channel LiDAR input takes the K = 64
-    # form from NCHW (its three zero channels dropped) against K = 224 from NHWC4: the same products summed in
-    # another order - within f16x3 / bf16 accumulation rounding
-    assert np.array_equal(a, b)
-    assert float(np.abs(a - ref).max()) <= 1e-5
-    (pi, pl), (ri, rl) = pools, ref_pools
-    assert np.array_equal(pi[: ri.size], ri[: pi.size])
-    n = min(pl.size, rl.size)
-    assert float(np.abs(pl[:n] - rl[:n]).max()) <= 2e-6 * max(1.0, float(np.abs(rl[:n]).max()))
+    assert np.array_equal(a, ref) and np.array_equal(b, ref)
+    for p, r in zip(pools, ref_pools):
+        assert np.array_equal(p[: r.size], r[: p.size])
