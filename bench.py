@@ -229,14 +229,8 @@ def main():
     scenes_per_s = B * world * args.steps / elapsed
     torch.cuda.synchronize()
     traj_gpu = out[rank * B:(rank + 1) * B].detach().cpu().numpy()
-    # the gathered tensor holds every rank's shard in rank order: each rank checks its own slice against the
-    # trajectories it computed (bit for bit), and the ranks agree on the result (MIN over ranks)
-    gather_ok = bool(np.array_equal(traj_gpu, last_local[0].detach().cpu().numpy()))
+    gather_ok = gather_slices_ok(out, last_local[0], rank, B, dist, dev)
     gathered = out.detach().cpu().numpy()
-    if dist is not None:
-        t = torch.tensor([1 if gather_ok else 0], device=dev, dtype=torch.int32)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        gather_ok = bool(t.item())
     shard0_golden_l2 = golden_l2(gathered, args.arch, B, args.denoise_steps) if B == 64 else None
     num_flags = pl.numerics_flags()
     if num_flags:
@@ -600,6 +594,17 @@ def cpu_baseline(args, cfg, sd, inp):
     return rec, ref
 
 
+def gather_slices_ok(gathered, local, rank, B, dist=None, dev=None):
+    """The all_gather output holds every rank's shard in rank order: each rank checks its own slice against the
+    trajectories it computed (bit for bit), and the ranks agree on the result (MIN over ranks)."""
+    ok = bool(np.array_equal(gathered[rank * B:(rank + 1) * B].detach().cpu().numpy(), local.detach().cpu().numpy()))
+    if dist is not None:
+        t = torch.tensor([1 if ok else 0], device=dev, dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item())
+    return ok
+
+
 def plumbing(args, world, rank):
     """CPU stand-in for the multi-rank path (tests): gloo process group, the same ScenePlanner
     all_gather, barrier + max-over-ranks timing, rank-0 JSON. The step is a stand-in (zeros)."""
@@ -625,6 +630,7 @@ def plumbing(args, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ranks_seen = sorted({int(v) for v in out[:, 0, 0].tolist()})
+    gather_ok = gather_slices_ok(out, planner.fn(None, None), rank, B, dist if world > 1 else None)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(B * world * args.steps / el, 3), "unit": "scenes/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -632,7 +638,9 @@ def plumbing(args, world, rank):
                           "scaling": "weak", "vs_baseline": None, "dtype": "none",
                           "data": "plumbing test: stand-in step, no forward (CPU, gloo)",
                           "config": {"workload": "plumbing", "batch_per_gpu": B, "global_batch": B * world,
-                                     "gathered_rows": int(out.shape[0]), "ranks_seen": ranks_seen}}), flush=True)
+                                     "gathered_rows": int(out.shape[0]), "ranks_seen": ranks_seen},
+                          "gather_check": {"gathered_rows": int(out.shape[0]),
+                                           "every_rank_slice_equals_local": gather_ok}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -29,6 +29,8 @@ def test_gpus2_launches_two_ranks():
     assert j["config"]["global_batch"] == 8
     assert j["config"]["gathered_rows"] == 8
     assert j["config"]["ranks_seen"] == [0, 1]
+    # the bench's own gather check (bench.gather_slices_ok): every rank's slice equals its local step, agreed by MIN
+    assert j["gather_check"] == {"gathered_rows": 8, "every_rank_slice_equals_local": True}
     assert j["value"] > 0 and j["scaling"] == "weak"
 
 

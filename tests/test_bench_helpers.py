@@ -51,3 +51,13 @@ def test_value_proj_algo_bytes_counts_each_neighbourhood_pixel_once():
     taps[4:6] = [4096 + 64 * 10 + 10, 4096 + 64 * 10 + 11]
     got = b.value_proj_algo_bytes(taps, np.array([3, 2], np.int32), 2)
     assert got == (25 + 5) * 1024 + 9 * 256 * 256 * 4
+
+
+def test_gather_slices_ok_detects_a_wrong_slice():
+    """bench.gather_slices_ok on one rank: the rank's own slice of the gathered rows against its local output."""
+    import torch
+    b = _bench()
+    local = torch.full((4, 8, 3), 1.0)
+    gathered = torch.cat([torch.zeros(4, 8, 3), local, torch.full((4, 8, 3), 2.0)])
+    assert b.gather_slices_ok(gathered, local, 1, 4)
+    assert not b.gather_slices_ok(gathered, local, 0, 4)
