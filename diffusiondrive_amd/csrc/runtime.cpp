@@ -191,12 +191,13 @@ class Model {
   // fork / join events of one forward (reused across forwards: every record precedes its wait)
   std::vector<hipEvent_t> fj_ev;
   size_t fj_next = 0;
-  // Single-stream graphs by default. Two-stream graphs (DDMI_STREAMS=1 or dd_set_streams(h, 2)) are opt-in: the HIP
-  // runtime's graph launch (ROCm 7.2) reads past its candidate-stream list when the exec's internal branch streams
-  // share the launch stream's hardware queue, a host segfault that depends on the process's queue history (DESIGN.md
-  // section 4, Handle lifetime). Batches-in-flight lanes were single-stream already.
-  bool use_side = false;
-  int main_prio = 0;  // priority of st_main (DDMI_MAIN_PRIORITY)
+  // Two-stream graphs (DDMI_STREAMS=0 or dd_set_streams(h, 1): one stream). The HIP runtime's multi-stream graph
+  // launch (ROCm 7.2) reads past its candidate-stream list when the exec's internal branch streams share the launch
+  // stream's hardware queue; the branch streams are created at normal priority, so the handle's own (launch) stream
+  // is created at the device's greatest priority, whose hardware queues are a separate pool (DESIGN.md section 4,
+  // Handle lifetime). Batches-in-flight lanes are single-stream on their callers' streams.
+  bool use_side = true;
+  int main_prio = 0;  // priority of st_main: the device's greatest (DDMI_MAIN_PRIORITY=0: default priority)
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
   bool value_dedup = true;
@@ -291,15 +292,17 @@ class Model {
     }
     // default-priority streams: either one at the device's greatest priority measured 3-3.5 % slower
     // in the B = 64 bench graph, both at the least priority 33 % slower
-    // DDMI_MAIN_PRIORITY=1 (experiment): the handle's own (launch) stream at the device's greatest priority, whose
-    // hardware queues are a separate pool from the normal-priority ones the runtime gives a multi-stream exec's
-    // branch streams (Handle lifetime)
-    if (const char* e = getenv("DDMI_MAIN_PRIORITY"))
-      if (atoi(e) != 0) {
+    // the handle's own (launch) stream at the device's greatest priority: its hardware queues are a separate pool
+    // from the normal-priority ones the runtime gives a multi-stream exec's branch streams, so no branch stream
+    // shares the launch stream's queue (Handle lifetime); DDMI_MAIN_PRIORITY=0 for A/B
+    {
+      const char* e = getenv("DDMI_MAIN_PRIORITY");
+      if (!(e && atoi(e) == 0)) {
         int least = 0, greatest = 0;
         DD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
         main_prio = greatest;
       }
+    }
     st_main = pooled_stream(device, main_prio);
     st_side = pooled_stream(device);
     st = st_own = st_main;

@@ -44,16 +44,19 @@ def test_caller_stream_replay_matches_own_stream(gpu_model):
 
 
 def test_two_stream_graphs_in_a_fresh_process():
-    """The opt-in two-stream graphs (dd_set_streams(h, 2)) in a child process of their own: against the single-stream
-    graph (within 1e-5: the same kernels, another order), and after 16 clones in both modes came and went. A fresh
-    process because the HIP runtime's multi-stream graph launch faults with a history-dependent hardware-queue
-    assignment (Handle lifetime); a fault here fails this test, not the suite."""
+    """Two-stream graphs (dd_set_streams(h, 2)) in a child process of their own, launched from default-priority
+    handle streams ($DDMI_MAIN_PRIORITY=0, the configuration whose queue sharing faulted in long processes) and from
+    the default greatest-priority ones: against the single-stream graph (within 1e-5: the same kernels, another order),
+    and after 16 clones in both modes came and went (Handle lifetime)."""
     import os
     import subprocess
     import sys
     child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "two_stream_child.py")
-    r = subprocess.run([sys.executable, child], capture_output=True, text=True, timeout=400)
-    assert r.returncode == 0 and "two_stream_child: ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    for prio in ("0", "1"):
+        env = dict(os.environ, DDMI_MAIN_PRIORITY=prio)
+        r = subprocess.run([sys.executable, child], capture_output=True, text=True, timeout=400, env=env)
+        assert r.returncode == 0 and "two_stream_child: ok" in r.stdout, (prio, r.returncode, r.stdout[-2000:],
+                                                                         r.stderr[-2000:])
 
 
 @pytest.mark.parametrize("lanes", [2, 3])
