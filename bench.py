@@ -98,7 +98,7 @@ def parse():
     p.add_argument("--no-compare", action="store_true", help="skip the fp32 leg and the H2D-inclusive leg")
     p.add_argument("--in-flight", type=int, default=3,
                    help="batches in flight per GPU (InFlightPlanner lanes: single-stream handles on streams of their "
-                        "own); 1 = one two-stream forward at a time")
+                        "own); 1 = one forward at a time on a default handle")
     p.add_argument("--lane-streams", type=int, default=1, choices=[1, 2],
                    help="streams of each lane's captured forward when --in-flight > 1")
     p.add_argument("--cpu-plumbing", action="store_true",
@@ -274,16 +274,16 @@ def main():
                     "in_flight": args.in_flight, "traj": o2.detach().cpu().numpy()}
         pl.set_gemm_mode(args.gemm)
         if args.in_flight > 1:
-            # one batch at a time on lane 0 as a two-stream handle (the --in-flight 1 configuration)
-            model.set_streams(2)
+            # one batch at a time on lane 0 as a default (single-stream) handle (the --in-flight 1 configuration)
+            model.set_streams(1)
             for _ in range(3):
                 model.forward(feats, noise=noise, steps=args.denoise_steps)
             n1 = max(5, min(args.steps // 2, 60))
             _, dt1, _, _ = timed(lambda: model.forward(feats, noise=noise, steps=args.denoise_steps)["trajectory"], n1,
                                  lanes=1)
             one_at_a_time = {"value": round(B * n1 / dt1, 3), "ms_per_step": round(dt1 / n1 * 1e3, 3), "steps": n1,
-                             "note": "in_flight 1: one two-stream forward at a time (its ms_per_step is the batch "
-                                     "latency of that mode)"}
+                             "note": "in_flight 1: one forward at a time on a default (single-stream) handle (its "
+                                     "ms_per_step is the batch latency of that mode)"}
             model.set_streams(args.lane_streams)
         # PCIe-inclusive: inputs staged from pinned host memory every step (one device buffer set per lane)
         host = {k: torch.from_numpy(inp[k]).pin_memory() for k in keys}
@@ -354,7 +354,7 @@ def main():
             "in_flight_note": "batches in flight per GPU: InFlightPlanner lanes (handles with the same weights, each "
                               "a single-stream captured forward replayed on a stream of its own); consecutive steps "
                               "go to consecutive lanes; every step's forward runs whole inside the timed region. "
-                              "1 = one two-stream forward at a time",
+                              "1 = one forward at a time on a default (single-stream) handle",
             "gemm": args.gemm,
             "heads": False,
             "heads_note": "the timed forward is the waypoint path (trajectory out); the BEV-semantic and agent "

@@ -144,6 +144,13 @@ static hipStream_t pooled_stream(int device, int priority = 0) {
   return s;
 }
 
+static hipStream_t fresh_stream(int device, int priority) {
+  (void)device;
+  hipStream_t s = nullptr;
+  DD_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+  return s;
+}
+
 static void release_stream(int device, hipStream_t s, int priority = 0) {
   (void)hipStreamSynchronize(s);
   if (!stream_pool_on()) {
@@ -191,13 +198,16 @@ class Model {
   // fork / join events of one forward (reused across forwards: every record precedes its wait)
   std::vector<hipEvent_t> fj_ev;
   size_t fj_next = 0;
-  // Two-stream graphs (DDMI_STREAMS=0 or dd_set_streams(h, 1): one stream). The HIP runtime's multi-stream graph
-  // launch (ROCm 7.2) reads past its candidate-stream list when the exec's internal branch streams share the launch
-  // stream's hardware queue; the branch streams are created at normal priority, so the handle's own (launch) stream
-  // is created at the device's greatest priority, whose hardware queues are a separate pool (DESIGN.md section 4,
-  // Handle lifetime). Batches-in-flight lanes are single-stream on their callers' streams.
-  bool use_side = true;
-  int main_prio = 0;  // priority of st_main: the device's greatest (DDMI_MAIN_PRIORITY=0: default priority)
+  // Single-stream graphs by default; two-stream ones opt-in (dd_set_streams(h, 2), or DDMI_STREAMS=1 at dd_create).
+  // The HIP runtime's multi-stream graph launch (ROCm 7.2) reads past its candidate-stream list when the exec's
+  // internal branch streams share the launch stream's hardware queue; the branch streams are created at normal
+  // priority, so a two-stream handle launches from a stream at the device's greatest priority, whose hardware queues
+  // are a pool of their own (Handle lifetime). That segregation costs time (B = 1 f16x3:
+  // 5.27 ms against 3.22 at default priority and 4.46 single-stream; profiles/round4_y_launch_priority.txt), so
+  // single-stream is the default. Batches-in-flight lanes are single-stream on their callers' streams.
+  bool use_side = false;
+  int main_prio = 0;  // priority of st_main: high_prio while two-stream, default priority while single-stream
+  int high_prio = 0;  // the device's greatest stream priority (DDMI_MAIN_PRIORITY=0: default, =least: least)
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
   bool value_dedup = true;
@@ -242,6 +252,19 @@ class Model {
   void drop_graphs() {
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
     graphs.clear();
+  }
+  // re-take the handle's own stream at priority p between forwards (graph execs hold no stream). A raised-priority
+  // stream is destroyed, not pooled: an idle one left in the process slowed default-priority lanes by 6 %.
+  void set_own_priority(int p) {
+    if (p == main_prio) return;
+    DD_HIP_CHECK(hipStreamSynchronize(st_own));
+    if (main_prio != 0) {
+      DD_HIP_CHECK(hipStreamDestroy(st_own));
+    } else {
+      release_stream(device, st_own, 0);
+    }
+    main_prio = p;
+    st = st_main = st_own = main_prio != 0 ? fresh_stream(device, main_prio) : pooled_stream(device, 0);
   }
   uint64_t graph_gen = 0;
   uint64_t generation = 0;  // bumped whenever a workspace buffer is (re)allocated
@@ -295,19 +318,22 @@ class Model {
     // the handle's own (launch) stream at the device's greatest priority: its hardware queues are a separate pool
     // from the normal-priority ones the runtime gives a multi-stream exec's branch streams, so no branch stream
     // shares the launch stream's queue (Handle lifetime); DDMI_MAIN_PRIORITY=0 for A/B
+    // only while it runs two-stream graphs: the stream is taken at default priority and raised by the first
+    // two-stream forward, lowered again by dd_set_streams(h, 1) (an idle greatest-priority stream anywhere in the
+    // process measured 6 % slower at 3 single-stream lanes in flight, profiles/round4_x_priority_ab.txt)
     {
       const char* e = getenv("DDMI_MAIN_PRIORITY");
-      if (!(e && atoi(e) == 0)) {
+      if (!(e && strcmp(e, "0") == 0)) {
         int least = 0, greatest = 0;
         DD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        main_prio = greatest;
+        high_prio = (e && strcmp(e, "least") == 0) ? least : greatest;
       }
     }
-    st_main = pooled_stream(device, main_prio);
+    if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
+    st_main = pooled_stream(device, 0);
     st_side = pooled_stream(device);
     st = st_own = st_main;
     DD_TRACE("create model %p st_main=%p st_side=%p", (void*)this, (void*)st_main, (void*)st_side);
-    if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_COMPACT")) value_compact = atoi(e) != 0;
@@ -381,7 +407,11 @@ class Model {
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     for (auto& e : fj_ev) (void)hipEventDestroy(e);
-    if (st_main) release_stream(device, st_main, main_prio);
+    if (st_own && main_prio != 0) {
+      (void)hipStreamDestroy(st_own);
+    } else if (st_own) {
+      release_stream(device, st_own, 0);
+    }
     if (st_side) release_stream(device, st_side);
     if (num_flags) (void)hipFree(num_flags);
     if (in_tab) (void)hipFree(in_tab);
@@ -1975,6 +2005,7 @@ class Model {
                      int steps, const Outs& o, hipStream_t caller, uint64_t scene0) {
     DD_HIP_CHECK(hipSetDevice(device));
     DD_TRACE("forward_chunk B=%d steps=%d caller=%p use_side=%d", B, steps, (void*)caller, (int)use_side);
+    set_own_priority(use_side ? high_prio : 0);
     OnStream on(*this, caller);
     const bool heads = o.sem || o.ag_states || o.ag_labels;
     const uint64_t gen0 = generation;
@@ -2207,6 +2238,7 @@ int dd_set_streams(dd_handle* h, int n) {
     DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a graph replayed on a caller's stream may still run
     m.drop_graphs();  // captured with the other topology
     m.use_side = n == 2;
+    m.set_own_priority(m.use_side ? m.high_prio : 0);
   });
 }
 

@@ -364,10 +364,10 @@ class DiffusionDriveModel:
         _lib.check(self.lib.dd_set_graph(self.handle, int(on)), self.lib)
 
     def set_streams(self, n: int):
-        """2 (default): the captured forward runs its independent branches (LiDAR trunk, tf decoder, heads) on a
-        second stream, launched from the handle's greatest-priority own stream (Handle
-        lifetime); 1: one stream, and a forward called on a non-default stream runs on that stream itself
-        (dd_set_streams; the per-lane mode of InFlightPlanner)."""
+        """1 (default): one stream, and a forward called on a non-default stream runs on that stream itself (the
+        per-lane mode of InFlightPlanner); 2: the captured forward runs its independent branches (LiDAR trunk, tf
+        decoder, heads) on a second stream, launched from the handle's own stream raised to the device's greatest
+        priority (Handle lifetime; faster only in bf16 at small batches). dd_set_streams."""
         _lib.check(self.lib.dd_set_streams(self.handle, int(n)), self.lib)
 
     def stream_count(self) -> int:
@@ -394,8 +394,8 @@ class InFlightPlanner:
     lane). Consecutive forwards go to consecutive lanes, so one batch's low-occupancy phases (the one-workgroup-
     per-scene decoder megakernels, the GPT stages, kernel ramps and tails) overlap the next batches' trunks.
     Throughput rises, the latency of each batch grows; the results are those of a single-stream forward, lane for
-    lane bit-identical (tests/test_inflight_gpu.py). lanes = 1 is the plain two-stream handle on the caller's
-    stream. No reference counterpart (the reference runs one eager forward at a time).
+    lane bit-identical (tests/test_inflight_gpu.py). lanes = 1 is the plain handle (single-stream unless set
+    otherwise) on the caller's stream. No reference counterpart (the reference runs one eager forward at a time).
 
     Outputs are produced on the lane's stream: read them after ``synchronize()`` (or ``wait()``, which makes the
     current stream wait for every lane); each forward first waits for the work already queued on the current

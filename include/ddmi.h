@@ -138,12 +138,13 @@ int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long lon
 int dd_kernel_bytes(dd_handle* h, const char* kernel, double* bytes);
 /* Enable / disable hipGraph capture + replay of the forward (default on). */
 int dd_set_graph(dd_handle* h, int enable);
-/* Streams of the captured forward: 2 (default; $DDMI_STREAMS=0 at dd_create gives 1) = the LiDAR trunk, the tf
- * decoder and the optional heads on a second stream beside the rest, the graph launched from the handle's own
- * stream, which is created at the device's greatest priority (the HIP runtime of ROCm 7.2 faults launching a
- * multi-stream graph whose internal branch streams share the launch stream's hardware queue; the greatest-priority
- * queues are a pool of their own: DESIGN.md section 4, Handle lifetime); 1 = everything in order on one stream, and a
- * forward called on a non-default stream runs on that stream itself (no hand-off through the handle's own stream). The batches-in-flight mode: N single-stream handles driven from N caller streams keep N forwards
+/* Streams of the captured forward: 1 (default) = everything in order on one stream, and a forward called on a
+ * non-default stream runs on that stream itself (no hand-off through the handle's own stream); 2 ($DDMI_STREAMS=1 at
+ * dd_create gives it too) = the LiDAR trunk, the tf decoder and the optional heads on a second stream beside the rest,
+ * the graph launched from the handle's own stream raised to the device's greatest priority (the HIP runtime of ROCm
+ * 7.2 faults launching a multi-stream graph whose internal branch streams share the launch stream's hardware queue;
+ * the greatest-priority queues are a pool of their own: DESIGN.md section 4, Handle lifetime). That separation costs
+ * more than the second stream gains in f16x3 / fp32 (bf16 still gains at batch 1), hence the single-stream default. The batches-in-flight mode: N single-stream handles driven from N caller streams keep N forwards
  * in flight on one device, one hardware queue each (diffusiondrive_amd/model.py InFlightPlanner); such a handle runs
  * the decoder's value_proj without its K split (less work on a shared device; $DDMI_VPROJ_SPLITS overrides). No
  * reference counterpart (the reference runs one eager forward at a time). */

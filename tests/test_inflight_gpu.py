@@ -46,7 +46,7 @@ def test_caller_stream_replay_matches_own_stream(gpu_model):
 def test_two_stream_graphs_in_a_fresh_process():
     """Two-stream graphs (dd_set_streams(h, 2)) in a child process of their own, launched from default-priority
     handle streams ($DDMI_MAIN_PRIORITY=0, the configuration whose queue sharing faulted in long processes) and from
-    the default greatest-priority ones: against the single-stream graph (within 1e-5: the same kernels, another order),
+    the greatest-priority ones a two-stream handle takes by default: against the single-stream graph (within 1e-5: the same kernels, another order),
     and after 16 clones in both modes came and went (Handle lifetime)."""
     import os
     import subprocess

@@ -115,11 +115,11 @@ def test_runner_lanes_match_one_lane(gpu, seeded_sd):
         assert np.abs(three[t].poses - one[t].poses).max() <= 1e-5, t
     runner.close()
     assert runner._clones == []
-    # a handle the caller configured single-stream stays single-stream
-    agent._transfuser_model.set_streams(1)
+    # a handle the caller configured two-stream (opt-in) is two-stream again after the lanes
+    agent._transfuser_model.set_streams(2)
     torch.manual_seed(33)
     BatchedTrajectoryRunner(agent, batch_size=2, lanes=2).run(toks[:3], inputs.__getitem__)
-    assert agent._transfuser_model.stream_count() == 1
+    assert agent._transfuser_model.stream_count() == 2
     agent._transfuser_model.set_streams(found)
     torch.manual_seed(33)
     again = BatchedTrajectoryRunner(agent, batch_size=2).run(toks, inputs.__getitem__)

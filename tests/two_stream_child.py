@@ -34,6 +34,9 @@ def main():
             o = c.forward(feats, noise=nz)["trajectory"].cpu()
         assert float((o - ref).abs().max()) <= 1e-5, i
         c.close()
+    two.set_streams(1)  # lowers the launch stream's priority (the raised stream is destroyed) ...
+    two.forward(feats, noise=nz)
+    two.set_streams(2)  # ... and the next two-stream forward raises it again
     for _ in range(2):
         again = two.forward(feats, noise=nz)["trajectory"].cpu()
     assert torch.equal(again, out)

@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--c1-two-stream", action="store_true",
                     help="child mode: C1 batch-1 latency with the opt-in two-stream graph, one JSON line")
+    ap.add_argument("--c1-streams", type=int, default=2, choices=[1, 2], help="child mode's dd_set_streams value")
     a = ap.parse_args()
     from diffusiondrive_amd.config import TransfuserConfig
     from diffusiondrive_amd.model import DiffusionDriveModel
@@ -106,7 +107,7 @@ def main():
 
     if a.c1_two_stream:  # a fresh process of its own (Handle lifetime)
         m, feats, noise = setup("resnet34", 1)
-        m.set_streams(2)
+        m.set_streams(a.c1_streams)
         rows = {}
         for mode in ("f16x3", "bf16", "fp32"):
             m.set_gemm_mode(mode)
