@@ -98,7 +98,7 @@ def parse():
     p.add_argument("--no-compare", action="store_true", help="skip the fp32 leg and the H2D-inclusive leg")
     p.add_argument("--in-flight", type=int, default=3,
                    help="batches in flight per GPU (InFlightPlanner lanes: single-stream handles on streams of their "
-                        "own); 1 = one forward at a time on a default handle")
+                        "own); 1 = one forward at a time on a default (two-stream) handle")
     p.add_argument("--lane-streams", type=int, default=1, choices=[1, 2],
                    help="streams of each lane's captured forward when --in-flight > 1")
     p.add_argument("--cpu-plumbing", action="store_true",
@@ -239,7 +239,7 @@ def main():
 
     # ---- roofline of the dominant kernel: a profiled single-stream replay of the same workload
     # (HIP events around every launch on the stream it is issued to)
-    # (lane 0; the profiled replay is single-stream - handles are single-stream by default)
+    # (lane 0; a profiled forward runs eagerly on one stream whatever the handle's stream count)
     model.set_profiling(True)
     model.reset_stats()
     prof_steps = max(1, min(args.steps, 5))
@@ -274,16 +274,22 @@ def main():
                     "in_flight": args.in_flight, "traj": o2.detach().cpu().numpy()}
         pl.set_gemm_mode(args.gemm)
         if args.in_flight > 1:
-            # one batch at a time on lane 0 as a default (single-stream) handle (the --in-flight 1 configuration)
-            model.set_streams(1)
-            for _ in range(3):
-                model.forward(feats, noise=noise, steps=args.denoise_steps)
+            # one batch at a time on lane 0 as a default handle (two streams: single-stream graph segments joined by
+            # events; the --in-flight 1 configuration), then as a single-stream handle for comparison
             n1 = max(5, min(args.steps // 2, 60))
-            _, dt1, _, _ = timed(lambda: model.forward(feats, noise=noise, steps=args.denoise_steps)["trajectory"], n1,
-                                 lanes=1)
-            one_at_a_time = {"value": round(B * n1 / dt1, 3), "ms_per_step": round(dt1 / n1 * 1e3, 3), "steps": n1,
-                             "note": "in_flight 1: one forward at a time on a default (single-stream) handle (its "
-                                     "ms_per_step is the batch latency of that mode)"}
+            one = {}
+            for ns in (2, 1):
+                model.set_streams(ns)
+                for _ in range(3):
+                    model.forward(feats, noise=noise, steps=args.denoise_steps)
+                _, dt1, _, _ = timed(lambda: model.forward(feats, noise=noise, steps=args.denoise_steps)["trajectory"],
+                                     n1, lanes=1)
+                one[ns] = (round(B * n1 / dt1, 3), round(dt1 / n1 * 1e3, 3))
+            one_at_a_time = {"value": one[2][0], "ms_per_step": one[2][1], "steps": n1,
+                             "single_stream": {"value": one[1][0], "ms_per_step": one[1][1]},
+                             "note": "in_flight 1: one forward at a time on a default handle (two streams, captured as "
+                                     "single-stream graph segments joined by events; its ms_per_step is the batch "
+                                     "latency of that mode); single_stream: the same on a one-stream handle"}
             model.set_streams(args.lane_streams)
         # PCIe-inclusive: inputs staged from pinned host memory every step (one device buffer set per lane)
         host = {k: torch.from_numpy(inp[k]).pin_memory() for k in keys}
@@ -354,7 +360,7 @@ def main():
             "in_flight_note": "batches in flight per GPU: InFlightPlanner lanes (handles with the same weights, each "
                               "a single-stream captured forward replayed on a stream of its own); consecutive steps "
                               "go to consecutive lanes; every step's forward runs whole inside the timed region. "
-                              "1 = one forward at a time on a default (single-stream) handle",
+                              "1 = one forward at a time on a default (two-stream) handle",
             "gemm": args.gemm,
             "heads": False,
             "heads_note": "the timed forward is the waypoint path (trajectory out); the BEV-semantic and agent "

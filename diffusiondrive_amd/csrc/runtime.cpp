@@ -144,13 +144,6 @@ static hipStream_t pooled_stream(int device, int priority = 0) {
   return s;
 }
 
-static hipStream_t fresh_stream(int device, int priority) {
-  (void)device;
-  hipStream_t s = nullptr;
-  DD_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
-  return s;
-}
-
 static void release_stream(int device, hipStream_t s, int priority = 0) {
   (void)hipStreamSynchronize(s);
   if (!stream_pool_on()) {
@@ -198,16 +191,12 @@ class Model {
   // fork / join events of one forward (reused across forwards: every record precedes its wait)
   std::vector<hipEvent_t> fj_ev;
   size_t fj_next = 0;
-  // Single-stream graphs by default; two-stream ones opt-in (dd_set_streams(h, 2), or DDMI_STREAMS=1 at dd_create).
-  // The HIP runtime's multi-stream graph launch (ROCm 7.2) reads past its candidate-stream list when the exec's
-  // internal branch streams share the launch stream's hardware queue; the branch streams are created at normal
-  // priority, so a two-stream handle launches from a stream at the device's greatest priority, whose hardware queues
-  // are a pool of their own (Handle lifetime). That segregation costs time (B = 1 f16x3:
-  // 5.27 ms against 3.22 at default priority and 4.46 single-stream; profiles/round4_y_launch_priority.txt), so
-  // single-stream is the default. Batches-in-flight lanes are single-stream on their callers' streams.
-  bool use_side = false;
-  int main_prio = 0;  // priority of st_main: high_prio while two-stream, default priority while single-stream
-  int high_prio = 0;  // the device's greatest stream priority (DDMI_MAIN_PRIORITY=0: default, =least: least)
+  // Two streams by default (dd_set_streams(h, 1) or DDMI_STREAMS=0 at dd_create: one). A two-stream forward is
+  // captured as a Program of single-stream graph segments joined by event records / waits between their launches
+  // (below): no graph exec has branch streams, so the HIP runtime's multi-stream graph launch - which read past its
+  // candidate-stream list when a branch stream shared the launch stream's hardware queue (ROCm 7.2, DESIGN.md
+  // section 4, Handle lifetime) - is never used. Batches-in-flight lanes are single-stream on their callers' streams.
+  bool use_side = true;
   // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
   bool value_gather = true;
   bool value_dedup = true;
@@ -246,25 +235,33 @@ class Model {
   TfMkLayer* tf_mk_layers = nullptr;  // device copy of the 3 layers' megakernel parameters
   size_t dim_t_off = kNone;
   size_t mk_w_begin = 0, mk_w_end = 0;  // arena float range of the megakernel images (prefetched per forward)
-  // graph cache keyed by the forward's shape signature; every entry belongs to the current buffer
+  // A captured forward: single-stream graph segments and the event operations between them, replayed in order.
+  // A single-stream forward is one segment. A two-stream forward has one segment per maximal run of launches on one
+  // logical stream between fork / join points (stems, the 4 trunk stages, tf decoder, heads, trajectory head: ~20);
+  // each fork / join is an event record on one logical stream and a wait on the other, issued between the segment
+  // launches exactly where the eager forward issues them.
+  struct SegOp {
+    int kind;               // 0: launch ex on stream s; 1: record fj_ev[ev] on s; 2: stream s waits fj_ev[ev]
+    int s;                  // logical stream: 0 main, 1 side
+    hipGraphExec_t ex;
+    int ev;
+  };
+  struct Program {
+    std::vector<SegOp> ops;
+    int segments = 0;
+    int branched = 0;  // segments whose graph has more than one root (parallel branches): 0 by construction
+  };
+  // program cache keyed by the forward's shape signature; every entry belongs to the current buffer
   // generation (the cache is emptied when a workspace buffer is (re)allocated: graphs hold its pointers)
-  std::map<std::string, hipGraphExec_t> graphs;
-  void drop_graphs() {
-    for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
-    graphs.clear();
+  std::map<std::string, Program> programs;
+  static void destroy_program(Program& p) {
+    for (auto& op : p.ops)
+      if (op.kind == 0 && op.ex) (void)hipGraphExecDestroy(op.ex);
+    p.ops.clear();
   }
-  // re-take the handle's own stream at priority p between forwards (graph execs hold no stream). A raised-priority
-  // stream is destroyed, not pooled: an idle one left in the process slowed default-priority lanes by 6 %.
-  void set_own_priority(int p) {
-    if (p == main_prio) return;
-    DD_HIP_CHECK(hipStreamSynchronize(st_own));
-    if (main_prio != 0) {
-      DD_HIP_CHECK(hipStreamDestroy(st_own));
-    } else {
-      release_stream(device, st_own, 0);
-    }
-    main_prio = p;
-    st = st_main = st_own = main_prio != 0 ? fresh_stream(device, main_prio) : pooled_stream(device, 0);
+  void drop_graphs() {
+    for (auto& g : programs) destroy_program(g.second);
+    programs.clear();
   }
   uint64_t graph_gen = 0;
   uint64_t generation = 0;  // bumped whenever a workspace buffer is (re)allocated
@@ -313,22 +310,8 @@ class Model {
       DD_HIP_CHECK(hipMalloc(&tf_mk_layers, sizeof(h)));
       DD_HIP_CHECK(hipMemcpy(tf_mk_layers, h, sizeof(h), hipMemcpyHostToDevice));
     }
-    // default-priority streams: either one at the device's greatest priority measured 3-3.5 % slower
-    // in the B = 64 bench graph, both at the least priority 33 % slower
-    // the handle's own (launch) stream at the device's greatest priority: its hardware queues are a separate pool
-    // from the normal-priority ones the runtime gives a multi-stream exec's branch streams, so no branch stream
-    // shares the launch stream's queue (Handle lifetime); DDMI_MAIN_PRIORITY=0 for A/B
-    // only while it runs two-stream graphs: the stream is taken at default priority and raised by the first
-    // two-stream forward, lowered again by dd_set_streams(h, 1) (an idle greatest-priority stream anywhere in the
-    // process measured 6 % slower at 3 single-stream lanes in flight, profiles/round4_x_priority_ab.txt)
-    {
-      const char* e = getenv("DDMI_MAIN_PRIORITY");
-      if (!(e && strcmp(e, "0") == 0)) {
-        int least = 0, greatest = 0;
-        DD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        high_prio = (e && strcmp(e, "least") == 0) ? least : greatest;
-      }
-    }
+    // both streams at default priority (one at the device's greatest priority measured 3-3.5 % slower in the B = 64
+    // bench graph, both at the least priority 33 % slower)
     if (const char* e = getenv("DDMI_STREAMS")) use_side = atoi(e) != 0;
     st_main = pooled_stream(device, 0);
     st_side = pooled_stream(device);
@@ -373,6 +356,7 @@ class Model {
     }
     DD_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     DD_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+    DD_HIP_CHECK(hipEventRecord(ev_out, st_own));  // recorded once, so every later wait on it is well defined
     // diffusers DDIMScheduler(beta_schedule="scaled_linear") schedule, bit-exact to the float32
     // arithmetic PyTorch-CPU performs for it (transfuser_model_v2.py:447-451):
     //   betas = torch.linspace(sqrt(1e-4), sqrt(0.02), 1000, float32) ** 2
@@ -398,8 +382,8 @@ class Model {
   }
 
   ~Model() {
-    DD_TRACE("destroy model %p st_main=%p st_side=%p graphs=%zu", (void*)this, (void*)st_main, (void*)st_side,
-             graphs.size());
+    DD_TRACE("destroy model %p st_main=%p st_side=%p programs=%zu", (void*)this, (void*)st_main, (void*)st_side,
+             programs.size());
     if (ev_out) (void)hipEventSynchronize(ev_out);  // the last forward, also when it ran on a caller's stream
     if (st_main) (void)hipStreamSynchronize(st_main);
     if (st_side) (void)hipStreamSynchronize(st_side);
@@ -407,11 +391,7 @@ class Model {
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     for (auto& e : fj_ev) (void)hipEventDestroy(e);
-    if (st_own && main_prio != 0) {
-      (void)hipStreamDestroy(st_own);
-    } else if (st_own) {
-      release_stream(device, st_own, 0);
-    }
+    if (st_own) release_stream(device, st_own, 0);
     if (st_side) release_stream(device, st_side);
     if (num_flags) (void)hipFree(num_flags);
     if (in_tab) (void)hipFree(in_tab);
@@ -921,21 +901,77 @@ class Model {
   }
   // profiled runs stay on one stream: per-launch event timing needs launches that do not overlap
   bool sides() const { return use_side && !profiling; }
-  void fork(hipStream_t to = nullptr) {
+
+  // Segmented capture (capture_program): every launch goes to st_cap under stream capture; fork / join / side close
+  // the open segment (a single-stream graph of the launches since the last boundary, tagged with its logical stream),
+  // append the event operations and open the next segment.
+  bool seg_cap = false;
+  int seg_s = 0;
+  hipStream_t st_cap = nullptr;
+  Program* seg_prog = nullptr;
+  void seg_begin(int s) {
+    seg_s = s;
+    DD_HIP_CHECK(hipStreamBeginCapture(st_cap, hipStreamCaptureModeThreadLocal));
+  }
+  void seg_end() {
+    hipGraph_t g = nullptr;
+    DD_HIP_CHECK(hipStreamEndCapture(st_cap, &g));
+    size_t n = 0, roots = 0;
+    hipError_t e = hipGraphGetNodes(g, nullptr, &n);
+    if (e == hipSuccess) e = hipGraphGetRootNodes(g, nullptr, &roots);
+    if (e == hipSuccess && n > 0) {
+      if (roots > 1) ++seg_prog->branched;
+      hipGraphExec_t ex = nullptr;
+      e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+      if (e == hipSuccess) {
+        seg_prog->ops.push_back({0, seg_s, ex, -1});
+        ++seg_prog->segments;
+      }
+    }
+    (void)hipGraphDestroy(g);
+    DD_HIP_CHECK(e);
+  }
+  void seg_event(int from, int to) {
+    const int e = (int)fj_next;
+    (void)fj_event();
+    seg_prog->ops.push_back({1, from, nullptr, e});
+    seg_prog->ops.push_back({2, to, nullptr, e});
+  }
+  void fork() {
     if (!sides()) return;
+    if (seg_cap) {
+      seg_end();
+      seg_event(0, 1);
+      seg_begin(0);
+      return;
+    }
     hipEvent_t e = fj_event();
     DD_HIP_CHECK(hipEventRecord(e, st_main));
-    DD_HIP_CHECK(hipStreamWaitEvent(to ? to : st_side, e, 0));
+    DD_HIP_CHECK(hipStreamWaitEvent(st_side, e, 0));
   }
-  void join(hipStream_t from = nullptr) {
+  void join() {
     if (!sides()) return;
+    if (seg_cap) {
+      seg_end();
+      seg_event(1, 0);
+      seg_begin(0);
+      return;
+    }
     hipEvent_t e = fj_event();
-    DD_HIP_CHECK(hipEventRecord(e, from ? from : st_side));
+    DD_HIP_CHECK(hipEventRecord(e, st_side));
     DD_HIP_CHECK(hipStreamWaitEvent(st_main, e, 0));
   }
   template <class F>
-  void side(F&& f, hipStream_t on = nullptr) {
-    st = sides() ? (on ? on : st_side) : st_main;
+  void side(F&& f) {
+    if (seg_cap) {  // launches stay on st_cap; the segment is tagged with the side stream
+      seg_end();
+      seg_begin(1);
+      f();
+      seg_end();
+      seg_begin(0);
+      return;
+    }
+    st = sides() ? st_side : st_main;
     try {
       f();
     } catch (...) {
@@ -943,6 +979,42 @@ class Model {
       throw;
     }
     st = st_main;
+  }
+
+  // Capture the forward into p: one single-stream graph, or (two streams) the segmented program above.
+  void capture_program(int B, int steps, bool heads, Program& p) {
+    seg_prog = &p;
+    st_cap = st;
+    seg_cap = sides();
+    try {
+      seg_begin(0);
+      forward_body(B, steps, heads);
+      seg_end();
+    } catch (...) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st_cap, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        hipGraph_t dummy = nullptr;
+        if (hipStreamEndCapture(st_cap, &dummy) == hipSuccess && dummy) (void)hipGraphDestroy(dummy);
+      }
+      (void)hipGetLastError();
+      seg_cap = false;
+      seg_prog = nullptr;
+      destroy_program(p);
+      throw;
+    }
+    seg_cap = false;
+    seg_prog = nullptr;
+  }
+  void run_program(const Program& p) {
+    const hipStream_t ss[2] = {st_main, st_side};
+    for (const SegOp& op : p.ops) {
+      if (op.kind == 0)
+        DD_HIP_CHECK(hipGraphLaunch(op.ex, ss[op.s]));
+      else if (op.kind == 1)
+        DD_HIP_CHECK(hipEventRecord(fj_ev[op.ev], ss[op.s]));
+      else
+        DD_HIP_CHECK(hipStreamWaitEvent(ss[op.s], fj_ev[op.ev], 0));
+    }
   }
 
   template <class F>
@@ -1976,13 +2048,17 @@ class Model {
       launch_traj_loss_reduce(train_part + 2 * (size_t)B, train_loss_dev + 1, B, Q, P, cls_w, reg_w, caller);
       launch_add2(train_loss_dev, caller);
       if (loss) DD_HIP_CHECK(hipMemcpyAsync(loss, train_loss_dev, 3 * sizeof(float), hipMemcpyDeviceToDevice, caller));
+      // the reduction read the handle-wide partials: the handle's next forward waits for it (OnStream)
+      DD_HIP_CHECK(hipEventRecord(ev_out, caller));
     }
   }
 
   // Single-stream forwards (dd_set_streams(h, 1)) called on a non-default stream run on the CALLER's stream
   // itself: no hand-off through the handle's own stream, so N handles driven from N caller streams (N batches
   // in flight) occupy N hardware queues, not 2N (the device has 4 per process by default; streams beyond them
-  // share queues and serialise). Restores the handle's stream on exit.
+  // share queues and serialise). Restores the handle's stream on exit. Either way the forward is ordered after the
+  // handle's previous one (ev_out; it may have run - or reduced losses - on another caller's stream), since both
+  // use the same workspace.
   struct OnStream {
     Model& m;
     bool direct;
@@ -1990,10 +2066,12 @@ class Model {
       if (direct) {
         m.st_main = caller;
         m.st = caller;
+        DD_HIP_CHECK(hipStreamWaitEvent(caller, m.ev_out, 0));
       } else {
         // order the handle's stream after the caller's stream, run everything there, then hand back
         DD_HIP_CHECK(hipEventRecord(m.ev_in, caller));
         DD_HIP_CHECK(hipStreamWaitEvent(m.st, m.ev_in, 0));
+        DD_HIP_CHECK(hipStreamWaitEvent(m.st, m.ev_out, 0));
       }
     }
     ~OnStream() {
@@ -2005,7 +2083,6 @@ class Model {
                      int steps, const Outs& o, hipStream_t caller, uint64_t scene0) {
     DD_HIP_CHECK(hipSetDevice(device));
     DD_TRACE("forward_chunk B=%d steps=%d caller=%p use_side=%d", B, steps, (void*)caller, (int)use_side);
-    set_own_priority(use_side ? high_prio : 0);
     OnStream on(*this, caller);
     const bool heads = o.sem || o.ag_states || o.ag_labels;
     const uint64_t gen0 = generation;
@@ -2018,35 +2095,21 @@ class Model {
                             std::to_string(gemm_mode) + "/s" + std::to_string(schedule) +
                             (train ? (train_target ? "/train1" : "/train0") : "");
     if (use_graph && !profiling && known_shapes.count(key)) {
-      if (graph_gen != generation || graphs.size() > 8) {
+      if (graph_gen != generation || programs.size() > 8) {
         // an earlier replay may still run (on the caller's stream in direct mode): ev_out marks the last forward
         DD_HIP_CHECK(hipEventSynchronize(ev_out));
         drop_graphs();
         graph_gen = generation;
       }
-      auto it = graphs.find(key);
-      DD_TRACE("graph key %s cached=%d", key.c_str(), (int)(it != graphs.end()));
-      if (it == graphs.end()) {
-        hipGraph_t g;
-        hipGraphExec_t ex = nullptr;
-        DD_HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        try {
-          forward_body(B, steps, heads);
-        } catch (...) {
-          hipGraph_t dummy;
-          (void)hipStreamEndCapture(st, &dummy);
-          throw;
-        }
-        DD_TRACE("captured");
-        DD_HIP_CHECK(hipStreamEndCapture(st, &g));
-        DD_TRACE("end capture");
-        DD_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-        DD_TRACE("instantiated exec %p on st=%p (model %p)", (void*)ex, (void*)st, (void*)this);
-        DD_HIP_CHECK(hipGraphDestroy(g));
-        it = graphs.emplace(key, ex).first;
+      auto it = programs.find(key);
+      DD_TRACE("graph key %s cached=%d", key.c_str(), (int)(it != programs.end()));
+      if (it == programs.end()) {
+        Program p;
+        capture_program(B, steps, heads, p);
+        DD_TRACE("captured %d segments (model %p)", p.segments, (void*)this);
+        it = programs.emplace(key, std::move(p)).first;
       }
-      DD_TRACE("launch exec %p on st=%p (model %p)", (void*)it->second, (void*)st, (void*)this);
-      DD_HIP_CHECK(hipGraphLaunch(it->second, st));
+      run_program(it->second);
       DD_TRACE("launched");
     } else {
       // eager run (the first call for a shape allocates every buffer; later calls are captured)
@@ -2238,7 +2301,22 @@ int dd_set_streams(dd_handle* h, int n) {
     DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a graph replayed on a caller's stream may still run
     m.drop_graphs();  // captured with the other topology
     m.use_side = n == 2;
-    m.set_own_priority(m.use_side ? m.high_prio : 0);
+  });
+}
+
+int dd_graph_info(dd_handle* h, int* programs, int* segments, int* multi_stream_execs) {
+  return guarded([&] {
+    if (!h) throw std::invalid_argument("null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    int np = 0, ns = 0, nb = 0;
+    for (auto& kv : h->m->programs) {
+      ++np;
+      ns += kv.second.segments;
+      nb += kv.second.branched;
+    }
+    if (programs) *programs = np;
+    if (segments) *segments = ns;
+    if (multi_stream_execs) *multi_stream_execs = nb;
   });
 }
 

@@ -161,7 +161,8 @@ __global__ __launch_bounds__(256) void bev_ce_partial_kernel(const float* __rest
     float s = 0.f;
     for (int c = 0; c < C; ++c) s = s + expf(l[(int64_t)c * HW] - mx);
     const int t = target[i];
-    v = (logf(s) + mx) - l[(int64_t)t * HW];
+    // an id outside [0, C) (F.cross_entropy raises on it) poisons the loss instead of reading past the logits
+    v = t < C ? (logf(s) + mx) - l[(int64_t)t * HW] : __builtin_nanf("");
   }
   v = block_sum256(v, sh);
   if (threadIdx.x == 0) part[blockIdx.x] = v;

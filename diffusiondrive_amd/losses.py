@@ -67,9 +67,11 @@ def bev_semantic_loss(model, logits: torch.Tensor, target) -> torch.Tensor:
     tg = torch.as_tensor(target)
     if tuple(tg.shape) != (B, H, W):
         raise ValueError(f"bev_semantic_map target must be (B,{H},{W}), got {tuple(tg.shape)}")
+    # F.cross_entropy raises on a class id outside [0, C) (uint8 ids included); the kernel itself turns such an
+    # id into a NaN loss rather than reading past the logits
+    if tg.numel() and (int(tg.min()) < 0 or int(tg.max()) >= C):
+        raise ValueError(f"bev_semantic_map target ids must lie in [0, {C})")
     if tg.dtype != torch.uint8:
-        if int(tg.min()) < 0 or int(tg.max()) >= C:
-            raise ValueError(f"bev_semantic_map target ids must lie in [0, {C})")
         tg = tg.to(torch.uint8)
     tg = tg.to(logits.device).contiguous()
     lg = logits.contiguous()

@@ -248,7 +248,8 @@ class DiffusionDriveModel:
 
     def forward_train(self, features: Dict[str, torch.Tensor], targets: Optional[Dict[str, torch.Tensor]] = None,
                       timesteps: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
-                      heads: bool = True, stream: Optional[torch.cuda.Stream] = None) -> Dict[str, torch.Tensor]:
+                      heads: bool = True, stream: Optional[torch.cuda.Stream] = None,
+                      safe: bool = True) -> Dict[str, torch.Tensor]:
         """V2TransfuserModel.forward(features, targets) with the trajectory head in training mode
         (TrajectoryHead.forward_train, transfuser_model_v2.py:520-576) over the eval-mode network (dropout off,
         BatchNorm running statistics): the deterministic loss evaluator (dd_forward_train).
@@ -258,16 +259,40 @@ class DiffusionDriveModel:
         ``torch.randn``, :533-534). Returns ``trajectory`` (the last layer's argmax mode), ``poses_reg_list`` /
         ``poses_cls_list`` (every layer), ``timesteps`` / ``noise`` (the draws used) and, with ``targets``
         (``trajectory`` (B, 8, 3)), ``trajectory_loss`` and ``trajectory_loss_dict`` (LossComputer per layer,
-        modules/multimodal_loss.py:119-168) as 0-d tensors; ``heads`` adds the BEV-semantic / agent outputs."""
+        modules/multimodal_loss.py:119-168) as 0-d tensors; ``heads`` adds the BEV-semantic / agent outputs.
+        The outputs are ordered on the current stream when this returns (also with an explicit ``stream``).
+        ``safe`` (default): synchronise, and if a kernel raised a numerics flag (f16x3 activation beyond the fp16
+        range) re-run the call in fp32 with the same draws and warn, as ``forward(safe=True)`` does."""
         cfg = self.config
-        dev = torch.device(f"cuda:{self.device}")
-        s = stream or torch.cuda.current_stream(dev)
         B = torch.as_tensor(features["status_feature"]).shape[0]
         Q, P = cfg.num_modes, cfg.trajectory_sampling.num_poses
         if timesteps is None:
             timesteps = torch.randint(0, cfg.train_timestep_max, (B,))
         if noise is None:
             noise = torch.randn((B, Q, P, 2))
+        if not safe:
+            return self._forward_train(features, targets, timesteps, noise, heads, stream)
+        self.numerics_flags(clear=True)
+        res = self._forward_train(features, targets, timesteps, noise, heads, stream)
+        if self.numerics_flags(clear=True):
+            mode = self.gemm_mode()
+            warnings.warn(f"ddmi: numerics flag raised in gemm mode {mode!r}; re-running forward_train in fp32")
+            self.set_gemm_mode("fp32")
+            try:
+                res = self._forward_train(features, targets, timesteps, noise, heads, stream)
+            finally:
+                self.set_gemm_mode(mode)
+            if self.numerics_flags(clear=True):
+                raise _lib.DDMIError("numerics flag raised by the fp32 forward_train as well")
+        return res
+
+    def _forward_train(self, features, targets, timesteps, noise, heads, stream) -> Dict[str, torch.Tensor]:
+        cfg = self.config
+        dev = torch.device(f"cuda:{self.device}")
+        cur = torch.cuda.current_stream(dev)
+        s = stream or cur
+        B = torch.as_tensor(features["status_feature"]).shape[0]
+        Q, P = cfg.num_modes, cfg.trajectory_sampling.num_poses
         with torch.cuda.stream(s):
             cam = self._dev(features["camera_feature"])
             lid = self._dev(features["lidar_feature"])
@@ -310,6 +335,14 @@ class DiffusionDriveModel:
                                                  nz.data_ptr(), tt.data_ptr(), tg.data_ptr() if tg is not None else None,
                                                  B, float(cfg.trajectory_cls_weight), float(cfg.trajectory_reg_weight),
                                                  ctypes.byref(outs), s.cuda_stream), self.lib)
+        if s != cur:
+            # the outputs (the loss reduction last) were written on s: order the caller's stream after it, so a
+            # .cpu() / .item() on the current stream reads finished values
+            cur.wait_stream(s)
+            for t in [res["trajectory"], *res["poses_reg_list"], *res["poses_cls_list"], loss,
+                      res.get("bev_semantic_map"), res.get("agent_states"), res.get("agent_labels")]:
+                if t is not None:
+                    t.record_stream(cur)
         res["timesteps"] = torch.as_tensor(timesteps)
         res["noise"] = torch.as_tensor(noise)
         if loss is not None:
@@ -364,10 +397,10 @@ class DiffusionDriveModel:
         _lib.check(self.lib.dd_set_graph(self.handle, int(on)), self.lib)
 
     def set_streams(self, n: int):
-        """1 (default): one stream, and a forward called on a non-default stream runs on that stream itself (the
-        per-lane mode of InFlightPlanner); 2: the captured forward runs its independent branches (LiDAR trunk, tf
-        decoder, heads) on a second stream, launched from the handle's own stream raised to the device's greatest
-        priority (Handle lifetime; faster only in bf16 at small batches). dd_set_streams."""
+        """2 (default): the forward runs its independent branches (LiDAR trunk, tf decoder, heads) on a second
+        stream; it is captured as single-stream graph segments joined by events between their launches (no
+        multi-stream graph exec: DESIGN.md section 4, Handle lifetime). 1: one stream, and a forward called on a
+        non-default stream runs on that stream itself (the per-lane mode of InFlightPlanner). dd_set_streams."""
         _lib.check(self.lib.dd_set_streams(self.handle, int(n)), self.lib)
 
     def stream_count(self) -> int:
@@ -375,6 +408,13 @@ class DiffusionDriveModel:
         n = ctypes.c_int()
         _lib.check(self.lib.dd_get_streams(self.handle, ctypes.byref(n)), self.lib)
         return n.value
+
+    def graph_info(self) -> Dict[str, int]:
+        """The captured forwards the handle holds (dd_graph_info): ``programs``, their single-stream graph
+        ``segments`` in all, and ``multi_stream_execs`` (segments with parallel branches: always 0)."""
+        p, s, m = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.dd_graph_info(self.handle, ctypes.byref(p), ctypes.byref(s), ctypes.byref(m)), self.lib)
+        return {"programs": p.value, "segments": s.value, "multi_stream_execs": m.value}
 
     def reset_stats(self):
         _lib.check(self.lib.dd_reset_stats(self.handle), self.lib)
@@ -391,10 +431,10 @@ class DiffusionDriveModel:
 class InFlightPlanner:
     """N batches in flight on one device: N handles with the same weights, each a single-stream captured forward
     driven from a stream of its own (dd_set_streams(1): the graph replays on that stream, one hardware queue per
-    lane). Consecutive forwards go to consecutive lanes, so one batch's low-occupancy phases (the one-workgroup-
-    per-scene decoder megakernels, the GPT stages, kernel ramps and tails) overlap the next batches' trunks.
+    lane). Consecutive forwards go to consecutive lanes, so one batch's low-occupancy phases (the decoder
+    megakernels, the GPT stages, kernel ramps and tails) overlap the next batches' trunks.
     Throughput rises, the latency of each batch grows; the results are those of a single-stream forward, lane for
-    lane bit-identical (tests/test_inflight_gpu.py). lanes = 1 is the plain handle (single-stream unless set
+    lane bit-identical (tests/test_inflight_gpu.py). lanes = 1 is the plain handle (two-stream unless set
     otherwise) on the caller's stream. No reference counterpart (the reference runs one eager forward at a time).
 
     Outputs are produced on the lane's stream: read them after ``synchronize()`` (or ``wait()``, which makes the
@@ -424,19 +464,26 @@ class InFlightPlanner:
     def __len__(self):
         return len(self.lanes)
 
+    @property
+    def next_index(self) -> int:
+        """The lane the next ``next_lane()`` takes."""
+        return self._next
+
     @contextlib.contextmanager
     def next_lane(self):
         """The next lane's model with the current stream set to that lane's stream (which first waits for the
-        caller's stream); work issued inside (the forward, a collective on its outputs) is ordered on the lane."""
+        caller's stream); work issued inside (the forward, a collective on its outputs) is ordered on the lane.
+        The round-robin pointer advances only when the body finishes without an exception, so a failed launch
+        leaves the lane free for the next batch (the batched runner keeps one pending job per lane)."""
         i = self._next
-        self._next = (i + 1) % len(self.lanes)
         s = self.streams[i]
         if s is None:
             yield self.lanes[i]
-            return
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            yield self.lanes[i]
+        else:
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                yield self.lanes[i]
+        self._next = (i + 1) % len(self.lanes)
 
     def forward(self, features: Dict[str, torch.Tensor], noise: Optional[torch.Tensor] = None,
                 steps: Optional[int] = None, heads: bool = False, modes: bool = False) -> Dict[str, torch.Tensor]:

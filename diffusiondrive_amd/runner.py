@@ -124,14 +124,22 @@ class BatchedTrajectoryRunner:
                 except Exception as e:  # noqa: BLE001
                     self._fail(tokens, e)
                     continue
+                # pending jobs sit on the lanes before next_index in round-robin order (the pointer advances only
+                # after a successful launch), so when every lane is busy the oldest job is on the lane taken next:
+                # its flags are read and cleared before another forward runs there
                 if len(pending) == len(pl):
                     finish_oldest()
+                lane = pl.lanes[pl.next_index]
                 try:
                     with torch.no_grad(), pl.next_lane() as m:
                         s = torch.cuda.current_stream(m.device)  # the lane's stream (the caller's with one lane)
                         res = m.forward(feats, noise=noise, safe=False, stream=s)
                 except Exception as e:  # noqa: BLE001
                     self._fail(tokens, e)
+                    try:  # a partly issued forward may have raised flags: clear them before the lane's next batch
+                        lane.numerics_flags(clear=True)
+                    except Exception:  # noqa: BLE001 - the lane's next batch then fails on its own
+                        pass
                     continue
                 pending.append((tokens, feats, noise, res, m, s))
             while pending:

@@ -138,20 +138,24 @@ int dd_kernel_stats(dd_handle* h, const char* kernel, double* total_ms, long lon
 int dd_kernel_bytes(dd_handle* h, const char* kernel, double* bytes);
 /* Enable / disable hipGraph capture + replay of the forward (default on). */
 int dd_set_graph(dd_handle* h, int enable);
-/* Streams of the captured forward: 1 (default) = everything in order on one stream, and a forward called on a
- * non-default stream runs on that stream itself (no hand-off through the handle's own stream); 2 ($DDMI_STREAMS=1 at
- * dd_create gives it too) = the LiDAR trunk, the tf decoder and the optional heads on a second stream beside the rest,
- * the graph launched from the handle's own stream raised to the device's greatest priority (the HIP runtime of ROCm
- * 7.2 faults launching a multi-stream graph whose internal branch streams share the launch stream's hardware queue;
- * the greatest-priority queues are a pool of their own: DESIGN.md section 4, Handle lifetime). That separation costs
- * more than the second stream gains in f16x3 / fp32 (bf16 still gains at batch 1), hence the single-stream default. The batches-in-flight mode: N single-stream handles driven from N caller streams keep N forwards
- * in flight on one device, one hardware queue each (diffusiondrive_amd/model.py InFlightPlanner); such a handle runs
- * the decoder's value_proj without its K split (less work on a shared device; $DDMI_VPROJ_SPLITS overrides). No
- * reference counterpart (the reference runs one eager forward at a time). */
+/* Streams of the captured forward: 2 (default; $DDMI_STREAMS=0 at dd_create gives 1) = the LiDAR trunk, the tf
+ * decoder and the optional heads on the handle's second stream beside the rest. The forward is captured as a program
+ * of SINGLE-stream graph segments (one per run of launches between fork / join points) replayed on the two streams
+ * with event records / waits between the segment launches: no graph exec has internal branch streams (the HIP runtime
+ * of ROCm 7.2 faults launching a multi-stream graph whose branch streams share the launch stream's hardware queue:
+ * DESIGN.md section 4, Handle lifetime). 1 = everything in order on one stream, and a forward called on a non-default
+ * stream runs on that stream itself (no hand-off through the handle's own stream): the batches-in-flight mode, N such
+ * handles driven from N caller streams keep N forwards in flight on one device, one hardware queue each
+ * (diffusiondrive_amd/model.py InFlightPlanner); such a handle runs the decoder's value_proj without its K split (less
+ * work on a shared device; $DDMI_VPROJ_SPLITS overrides). No reference counterpart (the reference runs one eager
+ * forward at a time). */
 int dd_set_streams(dd_handle* h, int n);
 /* The handle's current stream count (1 or 2, as dd_set_streams sets it): lets a caller that switches a handle to
  * single-stream for batches in flight restore what it found (diffusiondrive_amd/runner.py). */
 int dd_get_streams(dd_handle* h, int* n);
+/* The captured forwards the handle holds: programs (one per shape / mode), their single-stream graph segments in all,
+ * and segments whose graph has parallel branches (more than one root node: a multi-stream exec; 0 by construction). */
+int dd_graph_info(dd_handle* h, int* programs, int* segments, int* multi_stream_execs);
 /* GEMM arithmetic of every conv / linear of the path:
  *   DD_GEMM_FP32   fp32-input MFMA (v_mfma_f32_32x32x2_f32), an exact fp32 fma chain;
  *   DD_GEMM_F16X3  3-product fp16 split on f16 MFMA (conv_x3.hip): each fp32 operand becomes

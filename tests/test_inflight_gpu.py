@@ -44,19 +44,37 @@ def test_caller_stream_replay_matches_own_stream(gpu_model):
 
 
 def test_two_stream_graphs_in_a_fresh_process():
-    """Two-stream graphs (dd_set_streams(h, 2)) in a child process of their own, launched from default-priority
-    handle streams ($DDMI_MAIN_PRIORITY=0, the configuration whose queue sharing faulted in long processes) and from
-    the greatest-priority ones a two-stream handle takes by default: against the single-stream graph (within 1e-5: the same kernels, another order),
-    and after 16 clones in both modes came and went (Handle lifetime)."""
+    """Two-stream forwards (the default: single-stream graph segments on two streams joined by events) in a child
+    process of their own: against the single-stream graph (within 1e-5: the same kernels, another order), the
+    training forward's per-layer poses and losses too, and after 16 clones in both modes came and went (DESIGN.md
+    section 4, Handle lifetime)."""
     import os
     import subprocess
     import sys
     child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "two_stream_child.py")
-    for prio in ("0", "1"):
-        env = dict(os.environ, DDMI_MAIN_PRIORITY=prio)
-        r = subprocess.run([sys.executable, child], capture_output=True, text=True, timeout=400, env=env)
-        assert r.returncode == 0 and "two_stream_child: ok" in r.stdout, (prio, r.returncode, r.stdout[-2000:],
-                                                                         r.stderr[-2000:])
+    r = subprocess.run([sys.executable, child], capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0 and "two_stream_child: ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+
+
+def test_default_handle_has_no_multi_stream_exec(seeded_sd):
+    """The default handle is two-stream, and what it replays is a program of single-stream graph segments: after
+    the eager first call and the captured second one, one program of more than one segment, none with parallel
+    branches (dd_graph_info counts the root nodes of every segment's graph before instantiation)."""
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0)
+    try:
+        assert m.stream_count() == 2
+        f, nz = _inputs(2, 9)
+        outs = [m.forward(f, noise=nz)["trajectory"].cpu() for _ in range(3)]
+        info = m.graph_info()
+        assert info["programs"] == 1 and info["segments"] > 4 and info["multi_stream_execs"] == 0, info
+        assert torch.equal(outs[1], outs[2])  # replays are deterministic
+        m.set_streams(1)
+        one = m.forward(f, noise=nz)["trajectory"].cpu()
+        assert float((one - outs[2]).abs().max()) <= 1e-5
+        m.forward(f, noise=nz)
+        assert m.graph_info() == {"programs": 1, "segments": 1, "multi_stream_execs": 0}
+    finally:
+        m.close()
 
 
 @pytest.mark.parametrize("lanes", [2, 3])

@@ -187,3 +187,86 @@ def test_runner_isolates_failures_per_batch(monkeypatch):
     assert sorted(got) == ["t0", "t1", "t8", "t9"]
     assert float(got["t9"].poses[0, 0]) == 9.0
     assert _Agent._transfuser_model.streams == 2  # untouched with one lane
+
+
+def test_runner_failed_launch_keeps_lanes_and_pending_aligned(monkeypatch):
+    """lanes = 2 and a batch whose forward launch raises: the lane pointer must not advance, so the next batch takes
+    the free lane and a lane never holds two pending forwards. Otherwise finishing the older forward would read and
+    clear the numerics flag of the newer one on the same lane, and an f16x3 overflow in the newer batch would come
+    back unflagged (never re-run in fp32). CPU: stand-in handles whose flag word is per lane."""
+    import contextlib
+
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.runner import BatchedTrajectoryRunner
+
+    class _Stream:
+        def __init__(self, *a, **k):
+            pass
+
+        def synchronize(self):
+            pass
+
+        def wait_stream(self, other):
+            pass
+
+    reruns = []
+
+    class _Model:
+        device = 0
+
+        def __init__(self):
+            self.streams, self.flag, self.busy = 2, 0, 0
+
+        def clone(self):
+            return _Model()
+
+        def stream_count(self):
+            return self.streams
+
+        def set_streams(self, n):
+            self.streams = n
+
+        def numerics_flags(self, clear=True):
+            f = self.flag
+            if clear:
+                self.flag, self.busy = 0, 0
+            return f
+
+        def forward(self, feats, noise=None, safe=False, stream=None):
+            tags = feats["tags"]
+            if "boom" in tags:
+                raise RuntimeError("forward launch failed")
+            assert self.busy == 0, "a lane took a second batch while its first was still pending"
+            self.busy = 1
+            if any(t.startswith("ovf") for t in tags):
+                self.flag = 1  # this forward overflowed in f16x3
+            return {"trajectory": torch.stack([torch.full((8, 3), float(t.lstrip("ovft"))) for t in tags])}
+
+        def rerun_fp32(self, feats, noise, *a, **k):
+            reruns.append(tuple(feats["tags"]))
+            return {"trajectory": torch.full((len(feats["tags"]), 8, 3), -1.0)}
+
+        def close(self):
+            pass
+
+    class _Builder:
+        def compute_features_batch(self, inputs):
+            return {"tags": list(inputs)}
+
+    class _Agent:
+        _config = TransfuserConfig()
+        _transfuser_model = _Model()
+
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a, **k: _Stream())
+    monkeypatch.setattr(torch.cuda, "Stream", _Stream)
+    monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
+    runner = BatchedTrajectoryRunner.__new__(BatchedTrajectoryRunner)
+    runner.agent, runner.batch_size, runner.lanes, runner._clones = _Agent(), 1, 2, []
+    runner.device, runner.builder, runner.failed = 0, _Builder(), []
+    toks = ["t0", "boom", "ovf2", "t3", "t4", "boom", "t6", "ovf7"]
+    got = runner.run(toks, lambda t: t)
+    assert sorted(t for t, _ in runner.failed) == ["boom", "boom"]
+    assert sorted(reruns) == [("ovf2",), ("ovf7",)], reruns
+    assert float(got["ovf2"].poses[0, 0]) == -1.0 and float(got["ovf7"].poses[0, 0]) == -1.0
+    assert float(got["t3"].poses[0, 0]) == 3.0 and float(got["t0"].poses[0, 0]) == 0.0
+    assert _Agent._transfuser_model.streams == 2  # restored after the lanes ran single-stream

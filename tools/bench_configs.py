@@ -83,9 +83,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "configs"))
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--c1-two-stream", action="store_true",
-                    help="child mode: C1 batch-1 latency with the opt-in two-stream graph, one JSON line")
-    ap.add_argument("--c1-streams", type=int, default=2, choices=[1, 2], help="child mode's dd_set_streams value")
+    ap.add_argument("--c1-child", action="store_true",
+                    help="child mode: C1 batch-1 latency with --c1-streams streams, one JSON line")
+    ap.add_argument("--c1-streams", type=int, default=1, choices=[1, 2], help="child mode's dd_set_streams value")
     a = ap.parse_args()
     from diffusiondrive_amd.config import TransfuserConfig
     from diffusiondrive_amd.model import DiffusionDriveModel
@@ -105,7 +105,7 @@ def main():
         feats = {k: torch.from_numpy(inp[k]).to(dev) for k in ("camera_feature", "lidar_feature", "status_feature")}
         return m, feats, torch.from_numpy(inp["noise"]).to(dev)
 
-    if a.c1_two_stream:  # a fresh process of its own (Handle lifetime)
+    if a.c1_child:  # a fresh process of its own
         m, feats, noise = setup("resnet34", 1)
         m.set_streams(a.c1_streams)
         rows = {}
@@ -267,16 +267,16 @@ def main():
                   "batch 64, f16x3:", "", "| path | ms / batch | scenes/s |", "|---|---|---|"]
     for k, v in e2e_rows.items():
         lines.append(f"| {k} | {v['ms_per_batch']} | {v['scenes_per_s']} |")
-    # C1 with the opt-in two-stream graph, in a child process (a runtime fault there loses only this table)
-    r2 = subprocess.run([sys.executable, os.path.abspath(__file__), "--c1-two-stream", "--steps", str(a.steps)],
-                        capture_output=True, text=True, timeout=600)
+    # C1 on a single-stream handle (the tables above use the default two-stream handle), in a child process
+    r2 = subprocess.run([sys.executable, os.path.abspath(__file__), "--c1-child", "--c1-streams", "1",
+                         "--steps", str(a.steps)], capture_output=True, text=True, timeout=600)
     two = [ln for ln in r2.stdout.splitlines() if ln.startswith("C1TWO ")]
-    lines += ["", "C1 batch-1 latency with the opt-in two-stream graph (dd_set_streams(h, 2); fresh process):", "",
-              "| gemm | ms / batch | scenes/s |", "|---|---|---|"]
+    lines += ["", "C1 batch-1 latency on a single-stream handle (dd_set_streams(h, 1); fresh process; the rows above "
+              "are the default two-stream handle):", "", "| gemm | ms / batch | scenes/s |", "|---|---|---|"]
     if r2.returncode == 0 and two:
         rows2 = json.loads(two[-1][6:])
-        res["configs"]["C1_batch1_latency_two_stream"] = {"arch": "resnet34", "batch": 1, "ddim_steps": 2,
-                                                          "streams": 2, "modes": rows2}
+        res["configs"]["C1_batch1_latency_single_stream"] = {"arch": "resnet34", "batch": 1, "ddim_steps": 2,
+                                                             "streams": 1, "modes": rows2}
         lines += [f"| {k} | {v['ms_per_batch']} | {v['scenes_per_s']} |" for k, v in rows2.items()]
     else:
         lines.append(f"| (child exited {r2.returncode}) | - | - |")
