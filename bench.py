@@ -175,22 +175,10 @@ def main():
     feats = {k: torch.from_numpy(inp[k]).to(dev) for k in keys}
     noise = torch.from_numpy(inp["noise"]).to(dev)
     planner = ScenePlanner(lambda f, nz: pl.forward(f, noise=nz, steps=args.denoise_steps)["trajectory"])
-    marks = []  # per step: (start, end) HIP events on the stream the step ran on
-
-    last_local = [None]  # this rank's own trajectories of the latest step (checked against its gathered slice)
-
-    def lane_step(body):
-        # the next lane: its forward and the all_gather of its trajectories on the lane's stream
-        with pl.next_lane() as m:
-            s = torch.cuda.current_stream(dev)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            local_traj = body(m, s)
-            o = planner.gather(local_traj)
-            e1.record(s)
-            marks.append((e0, e1))
-            last_local[0] = local_traj
-            return o
+    lane_steps = LaneSteps(pl, planner, lambda: torch.cuda.Event(enable_timing=True),
+                           lambda: torch.cuda.current_stream(dev))
+    marks = lane_steps.marks  # per step: (start, end) HIP events on the stream the step ran on
+    lane_step = lane_steps.step
 
     def step():
         # per-rank shard of the global batch (weak scaling) + one RCCL all_gather of trajectories
@@ -229,7 +217,7 @@ def main():
     scenes_per_s = B * world * args.steps / elapsed
     torch.cuda.synchronize()
     traj_gpu = out[rank * B:(rank + 1) * B].detach().cpu().numpy()
-    gather_ok = gather_slices_ok(out, last_local[0], rank, B, dist, dev)
+    gather_ok = gather_slices_ok(out, lane_steps.last_local, rank, B, dist, dev)
     gathered = out.detach().cpu().numpy()
     shard0_golden_l2 = golden_l2(gathered, args.arch, B, args.denoise_steps) if B == 64 else None
     num_flags = pl.numerics_flags()
@@ -600,6 +588,35 @@ def cpu_baseline(args, cfg, sd, inp):
     return rec, ref
 
 
+class LaneSteps:
+    """The timed step of the bench: the next lane of an InFlightPlanner runs ``body(model, stream)`` (the forward),
+    then the rank's trajectories are all-gathered (ScenePlanner.gather: one RCCL all_gather_into_tensor) on the same
+    lane stream, bracketed by two events recorded there. Every rank issues its collectives in step order whatever
+    lane a step takes, and no forward waits for a later collective, so lanes cannot deadlock the ring. The CPU
+    plumbing path (gloo, stand-in lanes) runs this same class."""
+
+    def __init__(self, pl, planner, new_event, current_stream):
+        self.pl, self.planner = pl, planner
+        self.new_event, self.current_stream = new_event, current_stream
+        self.marks = []        # per step: (start, end) events on the stream the step ran on
+        self.last_local = None  # this rank's own trajectories of the latest step (checked against its gathered slice)
+        self.issue = []         # per step: (lane index, the lane's stream) in issue order
+
+    def step(self, body):
+        i = self.pl.next_index
+        with self.pl.next_lane() as m:
+            s = self.current_stream()
+            e0, e1 = self.new_event(), self.new_event()
+            e0.record(s)
+            local = body(m, s)
+            o = self.planner.gather(local)
+            e1.record(s)
+            self.marks.append((e0, e1))
+            self.issue.append((i, s))
+            self.last_local = local
+            return o
+
+
 def gather_slices_ok(gathered, local, rank, B, dist=None, dev=None):
     """The all_gather output holds every rank's shard in rank order: each rank checks its own slice against the
     trajectories it computed (bit for bit), and the ranks agree on the result (MIN over ranks)."""
@@ -612,22 +629,84 @@ def gather_slices_ok(gathered, local, rank, B, dist=None, dev=None):
 
 
 def plumbing(args, world, rank):
-    """CPU stand-in for the multi-rank path (tests): gloo process group, the same ScenePlanner
-    all_gather, barrier + max-over-ranks timing, rank-0 JSON. The step is a stand-in (zeros)."""
+    """CPU stand-in for the multi-rank path (tests): gloo process group, bench's own LaneSteps over an InFlightPlanner
+    of ``--in-flight`` stand-in lanes (the real round-robin, the real ScenePlanner all_gather per step, the real
+    gather check), barrier + max-over-ranks timing, rank-0 JSON. A lane's forward is a stand-in that returns
+    rank * 1000 + step for its scenes and records which lane issued which step."""
     import torch.distributed as dist
     from diffusiondrive_amd.dist import ScenePlanner
+    from diffusiondrive_amd.model import InFlightPlanner
     if world > 1:
         dist.init_process_group("gloo")
         world = dist.get_world_size()
     B = args.batch
-    planner = ScenePlanner(lambda f, nz: torch.full((B, 8, 3), float(rank)))
+
+    class _Stream:  # a lane stream: records what was issued on it
+        def __init__(self, k):
+            self.k, self.log = k, []
+
+        def wait_stream(self, other):
+            pass
+
+        def synchronize(self):
+            pass
+
+    class _Event:
+        def record(self, s):
+            s.log.append("event")
+
+    class _Planner(InFlightPlanner):
+        cur = [None]
+
+        def _new_stream(self):
+            return _Stream(0)  # numbered below
+
+        def _current_stream(self):
+            return _Planner.cur[0] or _main
+
+        def _on_stream(self, s):
+            import contextlib
+
+            @contextlib.contextmanager
+            def ctx():
+                prev, _Planner.cur[0] = _Planner.cur[0], s
+                try:
+                    yield
+                finally:
+                    _Planner.cur[0] = prev
+            return ctx()
+
+    class _Lane:
+        device = 0
+
+        def __init__(self):
+            self.streams = 2
+
+        def set_streams(self, n):
+            self.streams = n
+
+    _main = _Stream(-1)
+    lanes_in = [_Lane() for _ in range(args.in_flight)]
+    pl = _Planner(models=lanes_in, lane_streams=args.lane_streams)
+    for k, st in enumerate(pl.streams):
+        if st is not None:
+            st.k = k
+    planner = ScenePlanner(None)
+    lanes = LaneSteps(pl, planner, _Event, pl._current_stream)
+    step_no = [0]
+
+    def body(m, s):
+        step_no[0] += 1
+        s.log.append(("forward", step_no[0]))
+        return torch.full((B, 8, 3), float(rank * 1000 + step_no[0]))
+
     for _ in range(args.warmup):
-        planner.gather(planner.fn(None, None))
+        lanes.step(body)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = planner.gather(planner.fn(None, None))
+        out = lanes.step(body)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -635,8 +714,12 @@ def plumbing(args, world, rank):
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    ranks_seen = sorted({int(v) for v in out[:, 0, 0].tolist()})
-    gather_ok = gather_slices_ok(out, planner.fn(None, None), rank, B, dist if world > 1 else None)
+    ranks_seen = sorted({int(v) // 1000 for v in out[:, 0, 0].tolist()})
+    # every rank's slice of the last gather came from the same step (collectives issued in step order on all ranks)
+    steps_seen = sorted({int(v) % 1000 for v in out[:, 0, 0].tolist()})
+    gather_ok = gather_slices_ok(out, lanes.last_local, rank, B, dist if world > 1 else None)
+    lane_order = [i for i, _ in lanes.issue]
+    lane_streams_ok = all((s is None and len(pl) == 1) or (s is not None and s.k == i) for i, s in lanes.issue)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(B * world * args.steps / el, 3), "unit": "scenes/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -644,7 +727,12 @@ def plumbing(args, world, rank):
                           "scaling": "weak", "vs_baseline": None, "dtype": "none",
                           "data": "plumbing test: stand-in step, no forward (CPU, gloo)",
                           "config": {"workload": "plumbing", "batch_per_gpu": B, "global_batch": B * world,
-                                     "gathered_rows": int(out.shape[0]), "ranks_seen": ranks_seen},
+                                     "gathered_rows": int(out.shape[0]), "ranks_seen": ranks_seen,
+                                     "in_flight": args.in_flight},
+                          "lanes": {"issue_order": lane_order, "each_step_on_its_lane_stream": lane_streams_ok,
+                                    "last_gather_steps": steps_seen,
+                                    "lane_stream_logs": [[e if isinstance(e, str) else list(e) for e in s.log]
+                                                         for s in pl.streams if s is not None]},
                           "gather_check": {"gathered_rows": int(out.shape[0]),
                                            "every_rank_slice_equals_local": gather_ok}}), flush=True)
     if world > 1:

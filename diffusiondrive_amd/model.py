@@ -457,9 +457,18 @@ class InFlightPlanner:
         if lanes > 1:
             for m in self.lanes:
                 m.set_streams(lane_streams)
-        self.streams = [torch.cuda.Stream(torch.device(f"cuda:{self.device}")) for _ in range(lanes)] \
-            if lanes > 1 else [None]
+        self.streams = [self._new_stream() for _ in range(lanes)] if lanes > 1 else [None]
         self._next = 0
+
+    # stream primitives (a CPU stand-in planner - bench.py --cpu-plumbing - overrides these three)
+    def _new_stream(self):
+        return torch.cuda.Stream(torch.device(f"cuda:{self.device}"))
+
+    def _current_stream(self):
+        return torch.cuda.current_stream(self.device)
+
+    def _on_stream(self, s):
+        return torch.cuda.stream(s)
 
     def __len__(self):
         return len(self.lanes)
@@ -480,8 +489,8 @@ class InFlightPlanner:
         if s is None:
             yield self.lanes[i]
         else:
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
+            s.wait_stream(self._current_stream())
+            with self._on_stream(s):
                 yield self.lanes[i]
         self._next = (i + 1) % len(self.lanes)
 
@@ -489,20 +498,20 @@ class InFlightPlanner:
                 steps: Optional[int] = None, heads: bool = False, modes: bool = False) -> Dict[str, torch.Tensor]:
         with self.next_lane() as m:
             return m.forward(features, noise=noise, steps=steps, heads=heads, modes=modes,
-                             stream=torch.cuda.current_stream(self.device))
+                             stream=self._current_stream())
 
     __call__ = forward
 
     def wait(self):
         """Make the current stream wait for every lane's queued work."""
-        cur = torch.cuda.current_stream(self.device)
+        cur = self._current_stream()
         for s in self.streams:
             if s is not None:
                 cur.wait_stream(s)
 
     def synchronize(self):
         for s in self.streams:
-            (s or torch.cuda.current_stream(self.device)).synchronize()
+            (s or self._current_stream()).synchronize()
 
     def set_gemm_mode(self, mode: str):
         for m in self.lanes:

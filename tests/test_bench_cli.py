@@ -46,3 +46,24 @@ def test_single_rank_plumbing():
     assert r.returncode == 0, r.stderr
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["n_gpus"] == 1 and j["config"]["global_batch"] == 2
+
+
+def test_gpus2_three_lanes_in_flight_plumbing():
+    """bench.py's lane path at --in-flight 3 over gloo with two ranks: the bench's own LaneSteps drives an
+    InFlightPlanner of three stand-in lanes (its real round-robin), every step all-gathers on its lane's stream, and
+    the bench's gather check holds. Each step's issue lands on the next lane in order, each lane's stream sees
+    [event, forward, event] per step in step order, and the last gather holds one step's rows from both ranks
+    (the ranks issue their collectives in the same step order, so lanes cannot cross-match the ring)."""
+    r = _run(["--gpus", "2", "--cpu-plumbing", "--in-flight", "3", "--steps", "7", "--warmup", "2", "--batch", "3"])
+    assert r.returncode == 0, r.stderr
+    j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert j["config"]["in_flight"] == 3 and j["config"]["ranks_seen"] == [0, 1]
+    lanes = j["lanes"]
+    assert lanes["issue_order"] == [i % 3 for i in range(9)]
+    assert lanes["each_step_on_its_lane_stream"] is True
+    assert lanes["last_gather_steps"] == [9]
+    for k, log in enumerate(lanes["lane_stream_logs"]):
+        steps = [e[1] for e in log if isinstance(e, list)]
+        assert steps == list(range(k + 1, 10, 3)), (k, log)
+        assert log == [x for s in steps for x in ("event", ["forward", s], "event")], (k, log)
+    assert j["gather_check"] == {"gathered_rows": 6, "every_rank_slice_equals_local": True}

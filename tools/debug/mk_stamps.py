@@ -10,7 +10,7 @@ from diffusiondrive_amd.model import DiffusionDriveModel
 from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
 cfg = TransfuserConfig()
 m = DiffusionDriveModel(cfg, seeded_state_dict(cfg, 0), device=0, gemm="f16x3")
-B = 64
+B = int(os.environ.get("DDMI_STAMP_B", "64"))
 inp = synthetic_inputs(B, 1234)
 feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
 nz = torch.from_numpy(inp["noise"]).cuda()
