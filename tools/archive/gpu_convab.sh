@@ -1,6 +1,6 @@
 #!/bin/bash
 # conv micro-benchmark A/B over environments (tools/micro/conv_bench; exact shape names):
-#   SHAPES="img.l2.3x3 lid.l3.3x3" tools/gpu_convab.sh "" "DDMI_X6_CFG=1" ...
+#   SHAPES="img.l2.3x3 lid.l3.3x3" tools/archive/gpu_convab.sh "" "DDMI_X6_CFG=1" ...
 # prints "[env] <shape> ms TF/s ..." per shape and environment
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-end evidence (the GPU suite and smoke: tools/gpu_suite.sh): the bench line, the rocprofv3 kernel
+# Round-end evidence (the GPU suite and smoke: tools/archive/gpu_suite.sh): the bench line, the rocprofv3 kernel
 # trace of the bench workload (single stream, in flight 1), then the PMC passes (tools/gpu_pmc_round2.sh).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out

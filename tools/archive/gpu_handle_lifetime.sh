@@ -1,6 +1,6 @@
 #!/bin/bash
 # The round-4 handle-lifetime investigation (profiles/round4_f_handle_lifetime.md) as one script:
-#   tools/gpu_handle_lifetime.sh <step> [env ...]
+#   tools/archive/gpu_handle_lifetime.sh <step> [env ...]
 # steps:
 #   order   the reproducing order (test_runner -> test_inflight_gpu -> test_agent), stream pool off; extra env applies
 #           (e.g. DDMI_STREAMS=1 to run it with the two-stream graphs that faulted)

@@ -13,4 +13,4 @@ timeout -k 10 300 env $P AMD_LOG_LEVEL=3 python tools/repro/handle_churn.py 2 0 
 rc=$?; echo "[prio log] rc=$rc"; grep -a "Number of allocated hardware queues\|Selected queue\|hipGraphInstantiate (\|hipStreamCreateWithPriority (" /tmp/prio_log.txt | sed 's/\x1b\[[0-9;]*m//g' | head -60 > gpurun_out/prio_queues.txt; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 env $P python -u -m pytest tests -v -m gpu -x -rf --timeout 300 --timeout-method thread > gpurun_out/prio_suite.log 2>&1
 rc=$?; echo "[prio suite] rc=$rc"; tail -2 gpurun_out/prio_suite.log; [ $rc -ne 0 ] && exit $rc
-STEPS=60 BENCH_EXTRA="--in-flight 1" bash tools/gpu_envab.sh "DDMI_NONE=0" "DDMI_STREAMS=1 DDMI_MAIN_PRIORITY=1" "DDMI_STREAMS=1" | tee gpurun_out/prio_envab.txt
+STEPS=60 BENCH_EXTRA="--in-flight 1" bash tools/archive/gpu_envab.sh "DDMI_NONE=0" "DDMI_STREAMS=1 DDMI_MAIN_PRIORITY=1" "DDMI_STREAMS=1" | tee gpurun_out/prio_envab.txt

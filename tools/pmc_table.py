@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel-instance PMC table from tools/gpu_pmc_sq.sh output dirs.
+"""Per-kernel-instance PMC table from tools/archive/gpu_pmc_sq.sh output dirs.
 
     python tools/pmc_table.py gpurun_out/sq1 gpurun_out/sq2 ... [--filter conv]
 """
