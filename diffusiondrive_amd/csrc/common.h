@@ -282,6 +282,12 @@ struct VprojArgs {
   int max_splits = 3;  // 1..3 (DDMI_VPROJ_SPLITS: tests / A/B)
   int max_wgs = 256;   // workgroup budget for (tiles x splits): the CUs not held by a concurrent kernel
   int nsplit = 1;      // 1: 256-channel tiles (K split up to max_splits); 2: two 128-channel halves, no K split
+  // nsplit 2: the union-staged kernel, then the gathered one for the tiles it flagged (fb: [tiles][2] words, zero
+  // between launches); union 0 = the gathered kernel for every tile (DDMI_VPROJ_UNION=0)
+  int union_stage = 1;
+  int umax = 1 << 30;  // union size above which a tile falls back (tests: DDMI_VPROJ_UMAX; the kernel's capacity rules)
+  unsigned* fb = nullptr;
+  int fb_only = 0;     // (set by launch_vproj) the gathered kernel computes only the flagged (tile, half) pairs
 };
 bool vproj_supported(int C, int Cout, int H, int W);
 size_t vproj_tiles(int B, int cap);

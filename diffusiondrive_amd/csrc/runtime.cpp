@@ -208,6 +208,10 @@ class Model {
   // unsplit sum); 1 = 256-channel tiles with the K split (one at a time 4972-5017 -> 5109 scenes/s with 2, 3 in
   // flight unchanged: profiles/round4_d_envab_if1.txt)
   int vproj_nsplit = 2;
+  // DDMI_VPROJ_UNION: 1 (default) = the two-half form stages each row tile's 3 x 3-neighbourhood union once per
+  // channel group (value_proj.hip vproj_union_kernel); 0 = every (row, tap) gathered per K chunk
+  bool vproj_union = true;
+  int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
@@ -327,6 +331,8 @@ class Model {
     }
     if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
+    if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
     // zeroed on the handle's own stream and waited for: ordered before any forward, on whichever stream it runs
     DD_HIP_CHECK(hipMemsetAsync(in_tab, 0, 4 * sizeof(float*), st_own));
@@ -719,6 +725,10 @@ class Model {
       v.max_splits = (use_side || vproj_splits_env) ? vproj_splits : 1;
       v.max_wgs = std::max(64, num_cus() - busy_cus);
       v.nsplit = vproj_nsplit;
+      v.union_stage = vproj_union ? 1 : 0;
+      v.umax = vproj_umax;
+      if (v.nsplit == 2 && v.union_stage)
+        v.fb = reinterpret_cast<unsigned*>(buf_zeroed("vproj_fb", 2 * ((vproj_tiles(B, MR / B) + 7) / 8 * 8)));
       launch("value_proj", fl, [&] { launch_vproj(v, st); });
       return;
     }

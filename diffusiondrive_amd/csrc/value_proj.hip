@@ -127,6 +127,16 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
+  if constexpr (NH > 1) {
+    // after the union-staged kernel: only the (tile, half) pairs it handed over (their flags cleared here)
+    if (a.fb_only) {
+      const int bq = blockIdx.x / (8 * NH), rq = blockIdx.x % (8 * NH);
+      const int f = (bq * 8 + rq % 8) * NH + rq / 8;
+      if (__hip_atomic_load(a.fb + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+      __syncthreads();  // every thread read the flag before it is cleared
+      if (threadIdx.x == 0) a.fb[f] = 0u;
+    }
+  }
   // ---- compacted rows: launch row m = the m-th live row over the scenes in order
   rowcount_prefix(a.counts, a.B, g_pre);
   const int total = g_pre[a.B];
@@ -380,6 +390,416 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
     }
 }
 
+// ==================================================================================================================
+// Union-staged form (the default of the two-half mode). The 256 rows of a row tile are distinct map pixels of one or
+// two scenes, sorted by (scene, pixel); their 3 x 3 neighbourhoods overlap heavily (at B = 64, ~600 distinct pixels
+// for the 2304 (row, tap) pairs of a tile). Instead of gathering every (row, tap) pair from L2 per K chunk, the
+// workgroup stages the UNION of the neighbourhoods once per 16-channel group - register-staged 16-B loads issued
+// one group ahead, split into fp16 hi / lo in registers, written as 64-B pixel rows [hi 16 | lo 16 halfs] into the
+// other of two union buffers - and the 9 taps read their A fragments from it through a per-(row, tap) union-slot
+// table (a neighbour outside the map reads a zero row). B (pre-split weights, K order (kh, kw, ci)) streams through a
+// 4-slot LDS ring by LDS-DMA three steps ahead, every vector-memory op inline asm with an exact vmcnt per step (as
+// conv_x6.hip). K walks (channel group g) x (tap t): 16 x 9 steps of k = 16, f16x3 products.
+//
+// The union: a bitmap over the tile's key range (key = scene * 4096 + pixel; rows sorted, so the neighbours of the
+// tile lie in [first - 65, last + 65]), prefix popcounts, union slot = rank of the key (sorted, deterministic).
+// A tile whose range or union exceeds the staging capacity raises its fallback flag and returns; the gathered
+// kernel above (vproj_kernel<2>, launched right after with fb_only) computes exactly those tiles and clears the flags.
+namespace {
+constexpr int VU_BM = 256, VU_BN = 128, VU_WM = 4, VU_WN = 2, VU_TM = 2, VU_TN = 2;
+constexpr int VU_NW = VU_WM * VU_WN, VU_NT = 64 * VU_NW;
+constexpr int VU_UMAX = 704;                           // union rows per buffer; row VU_UMAX is a zero row
+constexpr int VU_UBYTES = (VU_UMAX + 1) * 64;          // one union buffer: 45120 B
+constexpr int VU_BIMG = VU_BN * 32;                    // one B image of a ring slot: 128 rows x 16 k x 2 B
+constexpr int VU_BSLOT = 2 * VU_BIMG;                  // 8 KB
+constexpr int VU_D = 3, VU_NSLOT = 4;                  // DMA lead (steps), ring slots
+constexpr int VU_BQ = VU_BN / 32;                      // DMA instructions (32 rows of 32 B) per image per step
+constexpr int VU_BPS = 2 * VU_BQ / VU_NW;              // per wave per step
+constexpr int VU_ALD = ((VU_UMAX + 1) * 4 + VU_NT - 1) / VU_NT;  // union float4 loads per thread per group
+constexpr int VU_RBITS = 3 * 4096;                     // key range the bitmap covers (3 scenes)
+constexpr int VU_RW = VU_RBITS / 32;
+constexpr int VU_TA = 1, VU_TS = 7;                    // taps at which the next group's union is issued / stored
+constexpr int VU_NG = kC / 16;                         // channel groups
+constexpr int VU_LDS = 2 * VU_UBYTES + VU_NSLOT * VU_BSLOT;
+static_assert(VU_BPS >= 1 && (2 * VU_BQ) % VU_NW == 0 && VU_BQ % VU_BPS == 0, "B DMA split over the waves");
+static_assert(VU_NSLOT >= VU_D + 1, "ring");
+static_assert(VU_LDS <= 128 * 1024, "LDS");
+
+// 16-B slot swizzle of a 64-B union row: 16 consecutive rows at one logical slot hit 16 distinct bank groups
+__device__ inline int vu_swz(int u) { return (u >> 2) & 3; }
+
+// was a union load (issued at the open of tap VU_TA) issued after B(step t), i.e. at an open in [t - D, t - 1]?
+// The first group's union was loaded in the prologue, before every B DMA.
+constexpr bool vu_union_in_window(int t, bool first) {
+  for (int j = 1; j <= VU_D; ++j) {
+    const int u = t - j;
+    if (first && u < 0) return false;
+    if (((u % 9) + 9) % 9 == VU_TA) return true;
+  }
+  return false;
+}
+static_assert(VU_TA + VU_D < VU_TS, "the union loads leave every open window before their wait");
+
+template <int N>
+__device__ inline void vu_step_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+template <int N>
+__device__ inline void vu_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+typedef float vu_f4 __attribute__((ext_vector_type(4)));
+__device__ inline vu_f4 vu_vload(vp_i4 rsrc, uint32_t voff) {
+  vu_f4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
+  return v;
+}
+__device__ inline void vu_split4(const vu_f4 v, uint2& hi, uint2& lo) {
+  const vp_h2 h01 = __builtin_convertvector((vp_f2){v.x, v.y}, vp_h2);
+  const vp_h2 h23 = __builtin_convertvector((vp_f2){v.z, v.w}, vp_h2);
+  const vp_f2 f01 = __builtin_convertvector(h01, vp_f2);
+  const vp_f2 f23 = __builtin_convertvector(h23, vp_f2);
+  const vp_h2 l01 = __builtin_convertvector((vp_f2){v.x - f01.x, v.y - f01.y}, vp_h2);
+  const vp_h2 l23 = __builtin_convertvector((vp_f2){v.z - f23.x, v.w - f23.y}, vp_h2);
+  hi = make_uint2(__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23));
+  lo = make_uint2(__builtin_bit_cast(uint32_t, l01), __builtin_bit_cast(uint32_t, l23));
+}
+}  // namespace
+
+__global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
+  __shared__ __attribute__((aligned(1024))) char lds[VU_LDS];
+  __shared__ int g_rows[VU_BM];   // output row (scene b's l-th pixel: b * cap + l) of each tile row, -1 = none
+  __shared__ int g_key[VU_BM];    // its key (scene * 4096 + pixel), -1 = none
+  __shared__ unsigned g_bm[VU_RW];
+  __shared__ int g_wpre[VU_RW + 1];
+  __shared__ int g_upix[VU_UMAX];  // key of each union slot
+  __shared__ int g_pre[257];
+  __shared__ int g_usize;
+  const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // ---- tile: the two 128-channel halves of row tile mt take blocks with equal blockIdx % 8 (one XCD)
+  const int gq = blockIdx.x / 16, rq = blockIdx.x % 16;
+  const int nh = rq / 8, mt = gq * 8 + rq % 8;
+  rowcount_prefix(a.counts, a.B, g_pre);
+  const int total = g_pre[a.B];
+  const int tiles = (total + VU_BM - 1) / VU_BM;
+  if (mt >= tiles) return;  // workgroup-uniform
+  const int m0 = mt * VU_BM, n0 = nh * VU_BN;
+  for (int r = tid; r < VU_BM; r += VU_NT) {
+    const int g = m0 + r;
+    int idx = -1, key = -1;
+    if (g < total) {
+      int lo = 0, hi = a.B - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (g_pre[mid] <= g) lo = mid; else hi = mid - 1;
+      }
+      idx = lo * a.cap + (g - g_pre[lo]);
+      key = a.rows[idx];
+    }
+    g_rows[r] = idx;
+    g_key[r] = key;
+  }
+  __syncthreads();
+  // ---- the union of the rows' 3 x 3 neighbourhoods: bitmap over [key(first) - 65, key(last) + 65]
+  const int nrow = min(VU_BM, total - m0);
+  const int kbase = g_key[0] - 65;
+  const int range = g_key[nrow - 1] + 66 - kbase;
+  if (range > VU_RBITS) {
+    if (tid == 0) a.fb[mt * 2 + nh] = 1u;  // the gathered kernel computes this tile
+    return;
+  }
+  const int nwords = (range + 31) >> 5;
+  for (int w = tid; w < nwords; w += VU_NT) g_bm[w] = 0u;
+  __syncthreads();
+  if (tid < nrow) {
+    const int key = g_key[tid], p = key & 4095, y = p >> 6, x = p & 63;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      if ((unsigned)yy < (unsigned)kHW && (unsigned)xx < (unsigned)kHW) {
+        const int k = key + (t / 3 - 1) * kHW + (t % 3 - 1) - kbase;
+        atomicOr(&g_bm[k >> 5], 1u << (k & 31));
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive prefix of the words' popcounts (<= 384 words: 6 per lane)
+    constexpr int PL = (VU_RW + 63) / 64;
+    int c[PL], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int w = PL * tid + j;
+      c[j] = w < nwords ? __builtin_popcount(g_bm[w]) : 0;
+      sum += c[j];
+    }
+    int inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (tid >= o) inc += v;
+    }
+    int run = inc - sum;
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int w = PL * tid + j;
+      if (w <= VU_RW) g_wpre[w] = run;
+      run += c[j];
+    }
+    if (tid == 63) g_usize = run;
+  }
+  __syncthreads();
+  const int U = g_usize;
+  if (U > VU_UMAX || U > a.umax) {
+    if (tid == 0) a.fb[mt * 2 + nh] = 1u;
+    return;
+  }
+  for (int w = tid; w < nwords; w += VU_NT) {
+    unsigned bits = g_bm[w];
+    int slot = g_wpre[w];
+    while (bits) {
+      const int b = __builtin_ctz(bits);
+      bits &= bits - 1;
+      g_upix[slot++] = kbase + w * 32 + b;
+    }
+  }
+  // the zero rows (neighbours outside the map) of both union buffers
+  if (tid < 32) reinterpret_cast<uint32_t*>(lds + (tid >> 4) * VU_UBYTES + VU_UMAX * 64)[tid & 15] = 0u;
+  __syncthreads();
+
+  const vp_i4 rin = vp_rsrc(a.map);
+  // ---- union staging: thread element e = tid + NT i -> union slot e >> 2, channels 4 (e & 3) .. of the group.
+  // Offsets come from the slot table in LDS at each issue; the LDS write addresses are recomputed at the store.
+  vu_f4 hr[VU_ALD];
+  auto union_issue = [&](int g) {
+    const bool gv = g < VU_NG;
+#pragma unroll
+    for (int i = 0; i < VU_ALD; ++i) {
+      const int e = tid + VU_NT * i, u = e >> 2;
+      const bool ok = gv && u < U;
+      const int o = ok ? g_upix[u] * kC + 4 * (e & 3) + g * 16 : 0;
+      hr[i] = vu_vload(rin, ok ? (uint32_t)o * 4u : kOOBv);
+    }
+  };
+  auto union_tie = [&]() {
+#pragma unroll
+    for (int i = 0; i < VU_ALD; ++i) asm volatile("" : "+v"(hr[i]));
+  };
+  auto union_store = [&](int buf) {
+    char* base = lds + buf * VU_UBYTES;
+#pragma unroll
+    for (int i = 0; i < VU_ALD; ++i) {
+      const int e = tid + VU_NT * i, u = e >> 2, q = e & 3;
+      if (u >= U) continue;
+      // hi: logical slot q >> 1, 8-B half q & 1; lo: logical slot + 2 (32 B further, before the swizzle)
+      const int w = u * 64 + ((((q >> 1) ^ vu_swz(u)) & 3) << 4) + ((q & 1) << 3);
+      uint2 hi, lo;
+      vu_split4(hr[i], hi, lo);
+      *reinterpret_cast<uint2*>(base + w) = hi;
+      *reinterpret_cast<uint2*>(base + (w ^ 32)) = lo;
+    }
+  };
+
+  // ---- B ring DMA: wave instruction j covers one image, rows rb .. rb+31 of the slot (32 B each, 16-B slot of
+  // lane l = l & 1 ^ (row >> 3) & 1)
+  uint32_t boff[VU_BPS];
+  int brow[VU_BPS];
+#pragma unroll
+  for (int j = 0; j < VU_BPS; ++j) {
+    const int qi = wave * VU_BPS + j;
+    const int rb = (qi % VU_BQ) * 32;
+    const int c = rb + (lane >> 1);
+    const int ls = (lane & 1) ^ ((c >> 3) & 1);
+    boff[j] = (uint32_t)((n0 + c) * a.ldh + ls * 8) * 2u;
+    brow[j] = rb;
+  }
+  const bool bimg_lo = (wave * VU_BPS) / VU_BQ == 1;
+  const vp_i4 rwb = vp_rsrc(bimg_lo ? (const void*)a.wl : (const void*)a.wh);
+  auto b_issue = [&](int slot, int tap, int g) {
+    const bool gv = g < VU_NG;
+    const uint32_t kb = (uint32_t)(tap * kC + g * 16) * 2u;
+#pragma unroll
+    for (int j = 0; j < VU_BPS; ++j) {
+      const uint32_t dst = lds_u32 + 2 * VU_UBYTES + slot * VU_BSLOT + (bimg_lo ? VU_BIMG : 0) + brow[j] * 32;
+      vp_dma(rwb, __builtin_amdgcn_readfirstlane(dst), gv ? boff[j] + kb : kOOBv);
+    }
+  };
+
+  // ---- fragment addresses. A of (row tile i, tap t): the lane's row's union slot, 16-bit pairs per tap
+  const int wm = wave / VU_WN, wn = wave % VU_WN;
+  const int li = lane & 31, hh = lane >> 5;
+  static_assert(VU_TM == 2, "slot pairs");
+  uint32_t uslot[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) uslot[t] = 0u;
+#pragma unroll
+  for (int i = 0; i < VU_TM; ++i) {
+    const int m = (wm * VU_TM + i) * 32 + li;
+    const int key = g_key[m];
+    const int p = key & 4095, y = p >> 6, x = p & 63;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      int u = VU_UMAX;
+      if (key >= 0 && (unsigned)yy < (unsigned)kHW && (unsigned)xx < (unsigned)kHW) {
+        const int k = key + (t / 3 - 1) * kHW + (t % 3 - 1) - kbase;
+        u = g_wpre[k >> 5] + __builtin_popcount(g_bm[k >> 5] & ((1u << (k & 31)) - 1u));
+      }
+      uslot[t] |= (uint32_t)u << (16 * i);
+    }
+  }
+  auto a_addr = [&](int i, int t) {  // hi 8 halfs of k 8 hh .. of the group (lo: ^ 32)
+    const int u = (int)((uslot[t] >> (16 * i)) & 0xffffu);
+    return u * 64 + (((hh ^ vu_swz(u)) & 3) << 4);
+  };
+  int bad_[VU_TN];
+#pragma unroll
+  for (int j = 0; j < VU_TN; ++j) {
+    const int c = (wn * VU_TN + j) * 32 + li;
+    bad_[j] = c * 32 + ((hh ^ ((c >> 3) & 1)) << 4);
+  }
+
+  vp_f16 acc[VU_TM][VU_TN];
+#pragma unroll
+  for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+    for (int j = 0; j < VU_TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  struct Frag {
+    vp_h8 ah[VU_TM], al[VU_TM], bh[VU_TN], bl[VU_TN];
+  };
+  Frag F0, F1;
+  auto load_frag = [&](Frag& F, int slot, int g, auto TAP) {
+    constexpr int t = decltype(TAP)::value;
+    const char* ubuf = lds + (g & 1) * VU_UBYTES;
+    const char* bbuf = lds + 2 * VU_UBYTES + slot * VU_BSLOT;
+#pragma unroll
+    for (int j = 0; j < VU_TN; ++j) {
+      F.bh[j] = *reinterpret_cast<const vp_h8*>(bbuf + bad_[j]);
+      F.bl[j] = *reinterpret_cast<const vp_h8*>(bbuf + VU_BIMG + bad_[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < VU_TM; ++i) {
+      const int o = a_addr(i, t);
+      F.ah[i] = *reinterpret_cast<const vp_h8*>(ubuf + o);
+      F.al[i] = *reinterpret_cast<const vp_h8*>(ubuf + (o ^ 32));
+    }
+  };
+  auto mfma_frag = [&](const Frag& F) {  // small terms first, the hi x hi term last
+#pragma unroll
+    for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+      for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[i], F.bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+      for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+      for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+  };
+
+  // Barrier opening step (g, t): this wave's B(g, t) DMAs have landed (vmcnt = memory ops issued after them: B of
+  // the next D - 1 steps, plus the union loads if they were issued in the D opens since), every wave's have, every
+  // wave's LDS reads and union stores retired (lgkmcnt(0)). Then B(s + D) into the slot of step s - 1 (all its reads
+  // retired), and at t == TA the next group's union loads.
+  int slot = 0;
+  auto open_step = [&](int g, auto TAP, auto FIRST) {
+    constexpr int t = decltype(TAP)::value;
+    constexpr bool first = decltype(FIRST)::value;
+    constexpr int N = (VU_D - 1) * VU_BPS + (vu_union_in_window(t, first) ? VU_ALD : 0);
+    vu_step_barrier<N>();
+    constexpr int tn = (t + VU_D) % 9;
+    int ns = slot + VU_D;
+    if (ns >= VU_NSLOT) ns -= VU_NSLOT;
+    b_issue(ns, tn, t + VU_D >= 9 ? g + 1 : g);
+    if constexpr (t == VU_TA) union_issue(g + 1);
+  };
+
+  // ---- prologue: union of group 0 -> buffer 0, B of steps 0 .. D-1, open step 0, its fragments
+  union_issue(0);
+#pragma unroll
+  for (int u = 0; u < VU_D; ++u) b_issue(u % VU_NSLOT, u, 0);
+  vu_wait_vm<VU_D * VU_BPS>();
+  union_tie();
+  union_store(0);
+  open_step(0, std::integral_constant<int, 0>(), std::true_type());
+  load_frag(F0, 0, 0, std::integral_constant<int, 0>());
+
+  // step s = (g, t), software pipelined: [open step s+1] [its fragment reads into the other set] [MFMAs of step s];
+  // at t == TS the next group's union (loaded since the open of tap TA) goes to the other buffer, whose last reads
+  // (group g - 1) retired long before
+  auto step = [&](int g, auto TAP, auto FIRST, Frag& Fc, Frag& Fn) {
+    constexpr int t = decltype(TAP)::value;
+    constexpr bool first = decltype(FIRST)::value;
+    constexpr int t1 = (t + 1) % 9;
+    const int g1 = t == 8 ? g + 1 : g;
+    if (++slot == VU_NSLOT) slot = 0;
+    if (g1 < VU_NG) {
+      open_step(g1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>());
+      load_frag(Fn, slot, g1, std::integral_constant<int, t1>());
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_frag(Fc);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (t == VU_TS) {
+      // the union of group g + 1 was issued when step TA opened; younger: B issued at the opens of taps TA+1 .. TS+1
+      vu_wait_vm<(VU_TS + 1 - VU_TA) * VU_BPS>();
+      union_tie();
+      union_store((g + 1) & 1);
+    }
+  };
+  // 9 steps of a group; the fragment sets alternate per step, so a group starting from set A leaves the next
+  // group's tap 0 in set Bf (9 is odd): groups run in pairs (A, Bf), (Bf, A)
+  auto group = [&](int g, auto FIRST, Frag& A, Frag& Bf) {
+    step(g, std::integral_constant<int, 0>(), FIRST, A, Bf);
+    step(g, std::integral_constant<int, 1>(), FIRST, Bf, A);
+    step(g, std::integral_constant<int, 2>(), FIRST, A, Bf);
+    step(g, std::integral_constant<int, 3>(), FIRST, Bf, A);
+    step(g, std::integral_constant<int, 4>(), FIRST, A, Bf);
+    step(g, std::integral_constant<int, 5>(), FIRST, Bf, A);
+    step(g, std::integral_constant<int, 6>(), FIRST, A, Bf);
+    step(g, std::integral_constant<int, 7>(), FIRST, Bf, A);
+    step(g, std::integral_constant<int, 8>(), FIRST, A, Bf);
+  };
+  static_assert(VU_NG % 2 == 0, "group pairs");
+  group(0, std::true_type(), F0, F1);
+  group(1, std::false_type(), F1, F0);
+  for (int g = 2; g < VU_NG; g += 2) {
+    group(g, std::false_type(), F0, F1);
+    group(g + 1, std::false_type(), F1, F0);
+  }
+  vu_step_barrier<0>();  // drain the trailing (all-OOB) DMAs and LDS reads
+
+  // ---- epilogue from the accumulators: scale, bias, ReLU, the value rows out
+  bool bad = false;
+  float sc[VU_TN], bias[VU_TN];
+#pragma unroll
+  for (int j = 0; j < VU_TN; ++j) {
+    const int col = n0 + (wn * VU_TN + j) * 32 + li;
+    sc[j] = a.wsinv[col];
+    bias[j] = a.bias[col];
+  }
+#pragma unroll
+  for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+    for (int j = 0; j < VU_TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (wm * VU_TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const int ri = g_rows[row];
+        bad |= ri >= 0 && !__builtin_isfinite(acc[i][j][r]);
+        if (ri >= 0) a.out[(int64_t)ri * kC + n0 + (wn * VU_TN + j) * 32 + li] = fmaxf(acc[i][j][r] * sc[j] + bias[j], 0.f);
+      }
+  if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+}
+
 bool vproj_supported(int C, int Cout, int H, int W) { return C == kC && Cout == kC && H == kHW && W == kHW; }
 
 size_t vproj_tiles(int B, int cap) { return ((size_t)B * cap + VP_BM - 1) / VP_BM; }
@@ -400,7 +820,16 @@ void launch_vproj(const VprojArgs& a, hipStream_t st) {
   if (a.nsplit == 2) {
     // two 128-channel halves per row tile, no K split: grid in groups of 8 tiles x 2 halves
     const size_t t8 = (vproj_tiles(a.B, a.cap) + 7) / 8 * 8;
-    hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, a);
+    if (a.union_stage) {
+      if (!a.fb) throw std::runtime_error("vproj: the union-staged form needs its fallback flags");
+      hipLaunchKernelGGL(vproj_union_kernel, dim3((unsigned)(t8 * 2)), dim3(VU_NT), 0, st, a);
+      DD_HIP_CHECK(hipGetLastError());
+      VprojArgs f = a;
+      f.fb_only = 1;  // tiles whose union did not fit: the gathered form
+      hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, f);
+    } else {
+      hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, a);
+    }
   } else {
     // every (tile, split) the kernel may pick: up to 3 splits of every possible tile
     const dim3 grid((unsigned)(vproj_tiles(a.B, a.cap) * 3));
