@@ -95,6 +95,13 @@ struct ConvArgs {
   int64_t pool_sn = 0, pool_sh = 0, pool_sw = 0;
   const float* pool_add = nullptr;
   int64_t pool_add_sh = 0, pool_add_sw = 0;
+  // Fused LayerNorm of the finished output rows (conv_x3's quad epilogue with one N tile spanning the row, Cout 64
+  // or 128; launch_conv_gemm reports it through last_conv_ln()): ln_out (the same row layout as out) receives
+  // LayerNorm(out row) * ln_g + ln_b with layernorm_v4's arithmetic and lane order (bit-identical to the separate
+  // launch). Not fused: ln_out untouched, last_conv_ln() false.
+  float* ln_out = nullptr;
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
 };
 constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
 
@@ -153,7 +160,7 @@ __device__ inline void rowcount_prefix(const int* counts, int n, int* pre) {
 }
 
 // Can epi_quads serve this launch? Every output / residual row starts 16-B aligned and Cout % 4 == 0.
-__device__ inline bool epi_quads_ok(const ConvArgs& a) {
+__host__ __device__ inline bool epi_quads_ok(const ConvArgs& a) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   auto st4 = [](int64_t s, int n) { return n == 1 || s % 4 == 0; };
   return a.Cout % 4 == 0 && al(a.out) && al(a.wsinv) && (!a.bias || al(a.bias)) && st4(a.out_sn, a.Nimg) &&
@@ -191,6 +198,13 @@ __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], ch
   if (nv) {
     scl = *reinterpret_cast<const f4_t*>(a.wsinv + nq) * a.alpha;
     if (a.bias) bia = *reinterpret_cast<const f4_t*>(a.bias + nq);
+  }
+  // fused LayerNorm (ConvArgs::ln_out): only when this tile spans the whole row
+  const bool ln = a.ln_out && BN == a.Cout && (QN == 16 || QN == 32 || QN == 64);
+  f4_t lg = {0.f, 0.f, 0.f, 0.f}, lb = {0.f, 0.f, 0.f, 0.f};
+  if (ln) {
+    lg = *reinterpret_cast<const f4_t*>(a.ln_g + nq);
+    lb = *reinterpret_cast<const f4_t*>(a.ln_b + nq);
   }
   bool bad = false;
 #pragma unroll
@@ -234,6 +248,29 @@ __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], ch
       // the in-flight and the one-at-a-time bench (profiles/round3_o_nt_stores_ab.txt); conv_x5 / conv_x3 shapes
       // alone 1-10 % faster on the conv micro-benchmark
       __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(a.out + oo[k] + nq));
+      if (ln) {
+        // LayerNorm of the finished row: the row is the QN consecutive lanes of this pass (QN = BN / 4 = Cout / 4 =
+        // layernorm_v4's LPR, VPL 1, lane sub = quad), so the sums, the xor tree and the rounding (no contraction)
+        // are layernorm_v4's: bit-identical to the separate launch. Dead rows are dead for the whole lane group.
+#pragma clang fp contract(off)
+        float s = 0.f;
+        s += (v.x + v.y) + (v.z + v.w);
+#pragma unroll
+        for (int o = QN / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        const float mean = s / (float)BN;
+        const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+        float q = 0.f;
+        q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+#pragma unroll
+        for (int o = QN / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        const float rstd = rsqrtf(q / (float)BN + 1e-5f);
+        f4_t o4;
+        o4.x = (v.x - mean) * rstd * lg.x + lb.x;
+        o4.y = (v.y - mean) * rstd * lg.y + lb.y;
+        o4.z = (v.z - mean) * rstd * lg.z + lb.z;
+        o4.w = (v.w - mean) * rstd * lg.w + lb.w;
+        *reinterpret_cast<f4_t*>(a.ln_out + oo[k] + nq) = o4;
+      }
     }
   }
   return bad;
@@ -254,6 +291,8 @@ void launch_set_ptrs(const float** tab, const float* a, const float* b, hipStrea
 const char* last_conv_kernel();
 bool last_conv_pooled();           // did the last launch_conv_gemm also write ConvArgs::pool_out?
 void set_last_conv_pooled(bool p);
+bool last_conv_ln();               // did the last launch_conv_gemm also write ConvArgs::ln_out?
+void set_last_conv_ln(bool p);
 // the kernel + tile configuration of the calling thread's last conv / GEMM launch, e.g.
 // "conv_x6<8,32,128,4,2>" (TH, TW, BN, wave grid), "conv_x5<256,256>", "conv_x3<128,128,f16x3>"
 const char* last_conv_config();

@@ -267,6 +267,7 @@ void set_last_conv_kernel(const char* k);  // conv_x3.hip
 
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st) {
   set_last_conv_pooled(false);
+  set_last_conv_ln(false);
   if (a.rowmap && !a.wh) throw std::runtime_error("conv_gemm: gathered rows need the f16x3 kernel (conv_x3)");
   if (a.wh) {
     launch_conv_x3(a, st);

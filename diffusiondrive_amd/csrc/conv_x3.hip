@@ -501,6 +501,9 @@ void set_last_conv_kernel(const char* k) { g_last_conv = k; }
 static thread_local bool g_last_pooled = false;
 bool last_conv_pooled() { return g_last_pooled; }
 void set_last_conv_pooled(bool p) { g_last_pooled = p; }
+static thread_local bool g_last_ln = false;
+bool last_conv_ln() { return g_last_ln; }
+void set_last_conv_ln(bool p) { g_last_ln = p; }
 static thread_local const char* g_last_cfg = "";
 const char* last_conv_config() { return g_last_cfg; }
 void set_last_conv_config(const char* c) { g_last_cfg = c; }
@@ -530,33 +533,50 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
     throw std::runtime_error("conv_x3: operand extent >= 2 GiB (split the batch)");
   if ((int64_t)a.Ho * a.out_sh >= (int64_t(1) << 31) || (int64_t)a.Ho * a.res_sh >= (int64_t(1) << 31))
     throw std::runtime_error("conv_x3: per-image output extent too large");
-  // default f16x3 path: 3x3 stride-1 convs on the halo-reuse direct kernel (conv_x6.hip), other
-  // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
-  if (a.rowmap) {
+  set_last_conv_ln(false);
+  // a fused LayerNorm of the output rows (ConvArgs::ln_out) needs one N tile spanning the row in the quad epilogue:
+  // 64 x 64 tiles at Cout 64, 64 x 128 at Cout 128 (the same K order per output as every other tile: the GEMM output
+  // is unchanged); otherwise the request is ignored and the caller runs its LayerNorm launch
+  if (a.ln_out && a.ln_g && a.ln_b && !a.rowmap && a.KH == 1 && a.KW == 1 && (a.Cout == 64 || a.Cout == 128) &&
+      epi_quads_ok(a)) {
     g_last_conv = "conv_x3";
-    launch_x3_cfg<2, 2, 2, 2, 1>(a, M, K, st);  // gathered rows: 128 x 128
+    set_last_conv_ln(true);
+    if (a.Cout == 64)
+      launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
+    else
+      launch_x3_cfg<2, 2, 1, 2>(a, M, K, st);  // 64 x 128
     return;
   }
-  if (launch_conv_x6(a, st)) {
+  ConvArgs b = a;
+  b.ln_out = nullptr;  // every other route ignores it
+  const ConvArgs& a0 = b;
+  // default f16x3 path: 3x3 stride-1 convs on the halo-reuse direct kernel (conv_x6.hip), other
+  // grids that fill the chip on the LDS-DMA implicit GEMM (conv_x5.hip), the rest here
+  if (a0.rowmap) {
+    g_last_conv = "conv_x3";
+    launch_x3_cfg<2, 2, 2, 2, 1>(a0, M, K, st);  // gathered rows: 128 x 128
+    return;
+  }
+  if (launch_conv_x6(a0, st)) {
     g_last_conv = "conv_x6";
     return;
   }
-  if (launch_conv_x5(a, M, K, st)) {
+  if (launch_conv_x5(a0, M, K, st)) {
     g_last_conv = "conv_x5";
     return;
   }
   g_last_conv = "conv_x3";
-  const int64_t t128 = ((M + 127) / 128) * (int64_t)((a.Cout + 127) / 128);
-  const bool generic = !(a.Cin % BK == 0 && a.KH * a.KW <= 32);
-  if (a.Cout <= 64) {
+  const int64_t t128 = ((M + 127) / 128) * (int64_t)((a0.Cout + 127) / 128);
+  const bool generic = !(a0.Cin % BK == 0 && a0.KH * a0.KW <= 32);
+  if (a0.Cout <= 64) {
     if (!generic && (M + 255) / 256 >= 256)
-      launch_x3_cfg<4, 1, 2, 2>(a, M, K, st);  // 256 x 64
+      launch_x3_cfg<4, 1, 2, 2>(a0, M, K, st);  // 256 x 64
     else
-      launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);  // 64 x 64
+      launch_x3_cfg<2, 2, 1, 1>(a0, M, K, st);  // 64 x 64
   } else if (t128 >= 512) {
-    launch_x3_cfg<2, 2, 2, 2>(a, M, K, st);    // 128 x 128
+    launch_x3_cfg<2, 2, 2, 2>(a0, M, K, st);    // 128 x 128
   } else {
-    launch_x3_cfg<2, 2, 1, 1>(a, M, K, st);    // 64 x 64
+    launch_x3_cfg<2, 2, 1, 1>(a0, M, K, st);    // 64 x 64
   }
 }
 

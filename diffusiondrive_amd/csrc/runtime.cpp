@@ -211,6 +211,7 @@ class Model {
   // DDMI_VPROJ_UNION: 1 (default) = the two-half form stages each row tile's 3 x 3-neighbourhood union once per
   // channel group (value_proj.hip vproj_union_kernel); 0 = every (row, tap) gathered per K chunk
   bool vproj_union = true;
+  bool ln_fold = true;  // DDMI_LN_FOLD=0: every GPT LayerNorm as its own launch (gemm_ln)
   int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
@@ -332,6 +333,7 @@ class Model {
     if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_LN_FOLD")) ln_fold = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
     // zeroed on the handle's own stream and waited for: ordered before any forward, on whichever stream it runs
@@ -1221,6 +1223,48 @@ class Model {
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
   }
 
+  // C = A W^T + bias + res, and (when the GEMM can fuse it: conv_x3's quad epilogue with one N tile per row, Cout 64
+  // or 128) Y = LayerNorm(C) in the same pass, bit-identical to ln(); returns whether Y was written (otherwise the
+  // caller runs ln()). DDMI_LN_FOLD=0: never fused.
+  bool gemm_ln(const Lin& L, const float* A, int64_t lda, int M, float* C, int64_t ldc, const float* res, int64_t ldr,
+               const LNp& p, float* Y) {
+    ConvArgs a;
+    a.in = A;
+    a.in_sn = (int64_t)M * lda;
+    a.in_sh = lda;
+    a.in_sw = 0;
+    a.H = M;
+    a.W = 1;
+    a.Cin = L.nin;
+    a.wgt = W(L.w);
+    a.ldb = L.nin;
+    a.bias = W(L.b);
+    a.res = res;
+    a.res_sn = (int64_t)M * ldr;
+    a.res_sh = ldr;
+    a.out = C;
+    a.out_sn = (int64_t)M * ldc;
+    a.out_sh = ldc;
+    a.out_sw = 0;
+    a.Nimg = 1;
+    a.Ho = M;
+    a.Wo = 1;
+    a.Cout = L.nout;
+    use_split(a, L.x3);
+    if (ln_fold && p.c == L.nout) {
+      a.ln_out = Y;
+      a.ln_g = W(p.g);
+      a.ln_b = W(p.b);
+    }
+    const double fl = 2.0 * M * (double)L.nout * L.nin;
+    bool fused = false;
+    launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] {
+      launch_conv_gemm(a, st);
+      fused = a.ln_out && last_conv_ln();
+    }, &a);
+    return fused;
+  }
+
   // C = A[:, 0:kn] W[:, k0:k0+kn]^T (+bias when with_bias) (+res) (relu): a K-slice of a Linear (the weight
   // rows keep their full stride; 16-B aligned slices only)
   void gemm_slice(const Lin& L, int k0, int kn, bool with_bias, const float* A, int64_t a_gs, int64_t a_rs, int G,
@@ -1372,8 +1416,12 @@ class Model {
     conv(l2i[i], LP, (int64_t)64 * Cl, (int64_t)8 * Cl, Cl, B, 8, 8, X + (size_t)nimg * C, (int64_t)T * C,
          (int64_t)8 * C, C, false, W(g.pos) + (size_t)nimg * C, 0, (int64_t)8 * C, C);
     const int M = B * T;
-    for (const GptBlockW& w : g.blocks) {
-      ln(w.ln1, X, C, Hb, C, M);
+    // Hb = ln1(x) before each block's qkv, ln2(x) before its MLP, ln_f(x) at the end. Where the GEMM producing x
+    // (proj, MLP-down) spans the row in one tile (C <= 128), its epilogue writes the LayerNorm too (gemm_ln)
+    bool hb_ready = false;  // Hb already holds ln1 of the next block (or ln_f after the last)
+    for (size_t bi = 0; bi < g.blocks.size(); ++bi) {
+      const GptBlockW& w = g.blocks[bi];
+      if (!hb_ready) ln(w.ln1, X, C, Hb, C, M);
       gemm(w.qkv, Hb, C, M, QKV, 3 * C);
       // softmax(Q K^T / sqrt(hs)) V per (scene, head), one fused launch (attention.hip): fp32 MFMA in the
       // fp32 mode, f16x3 MFMA in the f16x3 mode (two-way split scores) and the bf16 mode (three-way)
@@ -1381,12 +1429,13 @@ class Model {
                             ? 0
                             : (gemm_mode == DD_GEMM_BF16 ? 2 : 1);
       launch("attn", 4.0 * B * T * T * (double)C, [&] { launch_gpt_attention(QKV, B, T, C, 4, Y, aprec, st); });
-      gemm(w.proj, Y, C, M, X, C, false, X, C);  // x = x + proj(y)
-      ln(w.ln2, X, C, Hb, C, M);
+      if (!gemm_ln(w.proj, Y, C, M, X, C, X, C, w.ln2, Hb))  // x = x + proj(y); Hb = ln2(x)
+        ln(w.ln2, X, C, Hb, C, M);
       gemm(w.mlp0, Hb, C, M, MLP, 4 * C, true);
-      gemm(w.mlp2, MLP, 4 * C, M, X, C, false, X, C);  // x = x + mlp(ln2 x)
+      const LNp& nxt = bi + 1 < g.blocks.size() ? g.blocks[bi + 1].ln1 : g.lnf;
+      hb_ready = gemm_ln(w.mlp2, MLP, 4 * C, M, X, C, X, C, nxt, Hb);  // x = x + mlp(ln2 x); Hb = next LN(x)
     }
-    ln(g.lnf, X, C, Hb, C, M);  // Hb = ln_f(x): image tokens rows 0..255, lidar 256..319 per scene
+    if (!hb_ready) ln(g.lnf, X, C, Hb, C, M);  // Hb = ln_f(x): image tokens rows 0..255, lidar 256..319 per scene
     conv(i2l[i], Hb + (size_t)nimg * C, (int64_t)T * C, (int64_t)8 * C, C, B, 8, 8, LO, (int64_t)64 * Cl,
          (int64_t)8 * Cl, Cl, false);
     // the image branch after the last fusion is never read (the BEV path takes the LiDAR features:

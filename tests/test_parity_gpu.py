@@ -536,3 +536,41 @@ def test_nchw_stem_equals_nhwc4_stem(gpu_model, seeded_sd, monkeypatch, mode):
     assert np.array_equal(a, ref) and np.array_equal(b, ref)
     for p, r in zip(pools, ref_pools):
         assert np.array_equal(p[: r.size], r[: p.size])
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "bf16"])
+def test_gpt_layernorm_fold_is_bit_identical(gpu_model, seeded_sd, monkeypatch, mode):
+    """The GPT blocks' LayerNorms at C <= 128 (ln2 after proj, ln1 of the next block / ln_f after the MLP-down) are
+    written by the epilogue of the GEMM that produces their input (conv_x3's quad epilogue, one N tile per row,
+    layernorm_v4's lane order and rounding): the LayerNorm outputs and therefore the whole forward are bit-identical
+    to the separate launches (DDMI_LN_FOLD=0), and 8 LayerNorm launches per forward are gone."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 3
+    inp = synthetic_inputs(B, 53)
+    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"]).cuda()
+
+    def run(m):
+        m.set_profiling(True)
+        m.reset_stats()
+        out = m.forward(feats, noise=nz, modes=True)
+        n_ln = m.kernel_stats("layernorm")["launches"]
+        m.set_profiling(False)
+        return {k: v.cpu().numpy() for k, v in out.items()}, n_ln, m.tap("gpt_h").cpu().numpy()
+
+    gpu_model.set_gemm_mode(mode)
+    try:
+        fused, n_fused, h_fused = run(gpu_model)
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    monkeypatch.setenv("DDMI_LN_FOLD", "0")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm=mode)
+    try:
+        ref, n_ref, h_ref = run(m)
+    finally:
+        m.close()
+    for k in ref:
+        assert np.array_equal(fused[k], ref[k]), (mode, k)
+    assert np.array_equal(h_fused[: h_ref.size], h_ref[: h_fused.size])  # ln_f of the last scale's tokens
+    assert n_ref - n_fused == 8, (n_ref, n_fused)
