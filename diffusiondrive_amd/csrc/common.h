@@ -278,6 +278,9 @@ __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], ch
 #endif
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
 void launch_conv_x3(const ConvArgs& a, hipStream_t st);
+// Fused BasicBlock (basicblock.hip): c1 = conv1 (x -> intermediate, ReLU), c2 = conv2 (intermediate -> y, residual x,
+// ReLU, optional pool_out) of a 64-channel stride-1 block; false (nothing launched) when the shapes do not fit.
+bool launch_basicblock(const ConvArgs& c1, const ConvArgs& c2, hipStream_t st);
 // Fused stem conv 7x7/2 (Cin 4, Cout 64, f16x3) + bias + ReLU + maxpool 3x3/2 into pool_out (B,Hp,Wp,64)
 // (stem_pool.hip); false when `a` is not such a stem (then nothing is launched).
 // src (optional): the device word holding the address of the reference's NCHW input of src_c channels (read by the

@@ -212,6 +212,7 @@ class Model {
   // channel group (value_proj.hip vproj_union_kernel); 0 = every (row, tap) gathered per K chunk
   bool vproj_union = true;
   bool ln_fold = true;  // DDMI_LN_FOLD=0: every GPT LayerNorm as its own launch (gemm_ln)
+  bool bb_fuse = true;  // DDMI_BB_FUSE=0: layer-1 BasicBlocks as two conv_x6 launches (fused_block)
   int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
@@ -334,6 +335,7 @@ class Model {
     if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
     if (const char* e = getenv("DDMI_LN_FOLD")) ln_fold = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_BB_FUSE")) bb_fuse = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
     // zeroed on the handle's own stream and waited for: ordered before any forward, on whichever stream it runs
@@ -1180,6 +1182,33 @@ class Model {
     conv_c(c, in4, N, H, Wd, stem, true);
     launch("pool", 0, [&] { launch_maxpool3x3s2(stem, pool, N, hs, ws, c.cout, hp, wp, st); });
   }
+  // a stride-1 BasicBlock without downsample as one launch (basicblock.hip: f16x3, 64 channels, sides % 16 == 0);
+  // false (nothing launched, no pool request consumed) when it does not apply
+  template <class RP>
+  bool fused_block(const Block& blk, const float* x, int N, int H, int Wd, float* y, RP&& request_pool) {
+    const Conv &k1 = blk.c1, &k2 = blk.c2;
+    if (k1.cin != 64 || k1.cout != 64 || k2.cout != 64 || k1.k != 3 || k2.k != 3 || k1.stride != 1 || H % 16 ||
+        Wd % 16 || gemm_mode != DD_GEMM_F16X3)
+      return false;
+    const int64_t sn = (int64_t)H * Wd * 64, sh = (int64_t)Wd * 64;
+    ConvArgs a1 = conv_args(k1, x, sn, sh, 64, N, H, Wd, nullptr, sn, sh, 64, true, nullptr, 0, 0, 0);
+    if (!a1.wh || a1.prec != 0) return false;
+    const PoolSpec saved = pool_next;
+    const int saved_p = pool_next_p;
+    request_pool();
+    ConvArgs a2 = conv_args(k2, nullptr, sn, sh, 64, N, H, Wd, y, sn, sh, 64, true, x, sn, sh, 64);
+    const double fl = 2.0 * 2.0 * N * (double)H * Wd * 64.0 * 9.0 * k1.cin_real;
+    bool ok = false;
+    launch("basicblock", fl, [&] { ok = launch_basicblock(a1, a2, st); });
+    if (!ok) {  // give the pool request back to the two-launch path
+      pool_next = saved;
+      pool_next_p = saved_p;
+      return false;
+    }
+    pool_done = a2.pool_out && last_conv_pooled();
+    return true;
+  }
+
   // contiguous NHWC conv; returns output spatial size
   void conv_c(const Conv& c, const float* in, int N, int H, int Wd, float* out, bool relu, const float* res = nullptr) {
     const int Ho = (H + 2 * c.pad - c.k) / c.stride + 1, Wo = (Wd + 2 * c.pad - c.k) / c.stride + 1;
@@ -1347,7 +1376,9 @@ class Model {
         pool_next = *pool;
         pool_next_p = oh / pool->oh;
       };
-      if (!blk.bottleneck) {
+      if (!blk.bottleneck && bb_fuse && bs == 1 && !blk.has_ds && fused_block(blk, cur, B, ch, cw, y, request_pool)) {
+        // conv1 + conv2 + identity in one launch (basicblock.hip): the intermediate stays in LDS
+      } else if (!blk.bottleneck) {
         conv_c(blk.c1, cur, B, ch, cw, tmp2, true);
         request_pool();
         conv_c(blk.c2, tmp2, B, oh, ow, y, true, sc);

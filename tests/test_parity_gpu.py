@@ -574,3 +574,46 @@ def test_gpt_layernorm_fold_is_bit_identical(gpu_model, seeded_sd, monkeypatch, 
         assert np.array_equal(fused[k], ref[k]), (mode, k)
     assert np.array_equal(h_fused[: h_ref.size], h_ref[: h_fused.size])  # ln_f of the last scale's tokens
     assert n_ref - n_fused == 8, (n_ref, n_fused)
+
+
+def test_fused_basicblock_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
+    """Layer 1 of both trunks (stride-1 64-channel BasicBlocks) runs as one launch per block (basicblock.hip: conv1's
+    output for the 18 x 18 pixels conv2 reads kept in LDS): the stage outputs, the GPT tokens pooled from the last
+    block and the whole forward are bit-identical to the two conv_x6 launches per block (DDMI_BB_FUSE=0) - the same
+    products, K order and epilogue expressions, the intermediate split as conv_x6 splits its halo."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 3
+    inp = synthetic_inputs(B, 59)
+    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"]).cuda()
+    taps = ("img_s0_a", "lid_s0_a", "img_s0_b", "lid_s0_b")
+
+    def run(m):
+        m.set_profiling(True)
+        m.reset_stats()
+        out = m.forward(feats, noise=nz, modes=True)
+        launches = m.kernel_stats("basicblock")["launches"]
+        m.set_profiling(False)
+        res = {k: v.cpu().numpy() for k, v in out.items()}
+        res.update({t: m.tap(t).cpu().numpy() for t in taps})
+        return res, launches
+
+    gpu_model.set_gemm_mode("f16x3")
+    try:
+        fused, n_fused = run(gpu_model)
+        replay = {k: v.cpu().numpy() for k, v in gpu_model.forward(feats, noise=nz, modes=True).items()}
+    finally:
+        gpu_model.set_gemm_mode("fp32")
+    monkeypatch.setenv("DDMI_BB_FUSE", "0")
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+    try:
+        ref, n_ref = run(m)
+    finally:
+        m.close()
+    assert n_fused == 6 and n_ref == 0, (n_fused, n_ref)
+    for k in ref:
+        n = min(fused[k].size, ref[k].size)
+        assert np.array_equal(fused[k].reshape(-1)[:n], ref[k].reshape(-1)[:n]), k
+    for k in replay:
+        assert np.array_equal(replay[k], ref[k]), k  # the captured graph as well
