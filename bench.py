@@ -71,8 +71,9 @@ KERNEL_DESC = {
     "conv_x3": "conv_x3 (implicit-GEMM conv / GEMM, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
     "conv_x5": "conv_x5 (implicit-GEMM conv, LDS-DMA staging, 3-product fp16 split on v_mfma_f32_32x32x16_f16)",
     "conv_x6": "conv_x6 (halo-reuse direct 3x3 conv on v_mfma_f32_32x32x16_{f16 x3 | bf16})",
+    "basicblock": "basicblock (fused layer-1 BasicBlock: two 3x3 convs, the intermediate in LDS, f16x3 MFMA)",
 }
-CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm")
+CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm", "basicblock")
 OTHER_KERNELS = ("value_proj", "stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
                  "decoder", "tfdec", "bevproj", "misc")
 DTYPE = {

@@ -1032,7 +1032,7 @@ class Model {
   }
 
   template <class F>
-  void launch(const char* name, double flops, F&& f, const ConvArgs* shape = nullptr) {
+  void launch(const char* name, double flops, F&& f, const ConvArgs* shape = nullptr, double bytes = -1.0) {
     if (!profiling) {
       f();
       return;
@@ -1061,7 +1061,7 @@ class Model {
                std::to_string(c.stride) + " z=" + std::to_string(c.batch) + " HW=" + std::to_string(c.H) + "x" +
                std::to_string(c.W);
     }
-    pending.push_back({name, flops, shape ? conv_algo_bytes(*shape) : 0.0, a, b, detail});
+    pending.push_back({name, flops, bytes >= 0.0 ? bytes : (shape ? conv_algo_bytes(*shape) : 0.0), a, b, detail});
   }
 
   void collect() {
@@ -1199,7 +1199,10 @@ class Model {
     ConvArgs a2 = conv_args(k2, nullptr, sn, sh, 64, N, H, Wd, y, sn, sh, 64, true, x, sn, sh, 64);
     const double fl = 2.0 * 2.0 * N * (double)H * Wd * 64.0 * 9.0 * k1.cin_real;
     bool ok = false;
-    launch("basicblock", fl, [&] { ok = launch_basicblock(a1, a2, st); });
+    // algorithmic bytes: the block input once (conv1's input and conv2's residual), the output once, both convs'
+    // split weight images
+    const double by = 2.0 * N * (double)H * Wd * 64 * 4 + 2.0 * 9 * 64 * 64 * 4;
+    launch("basicblock", fl, [&] { ok = launch_basicblock(a1, a2, st); }, nullptr, by);
     if (!ok) {  // give the pool request back to the two-launch path
       pool_next = saved;
       pool_next_p = saved_p;
