@@ -212,7 +212,10 @@ class Model {
   // channel group (value_proj.hip vproj_union_kernel); 0 = every (row, tap) gathered per K chunk
   bool vproj_union = true;
   bool ln_fold = true;  // DDMI_LN_FOLD=0: every GPT LayerNorm as its own launch (gemm_ln)
-  bool bb_fuse = true;  // DDMI_BB_FUSE=0: layer-1 BasicBlocks as two conv_x6 launches (fused_block)
+  // DDMI_BB_FUSE=1: layer-1 BasicBlocks as one launch each (fused_block, basicblock.hip). Off by default: measured
+  // 2.37 ms per forward against 2.06 for the two conv_x6 launches per block (profiles/round5_c_bench.json: one
+  // workgroup per CU runs its phases back to back, 39.5 us per tile against ~16 us of MFMA work)
+  bool bb_fuse = false;
   int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward

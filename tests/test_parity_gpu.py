@@ -579,8 +579,9 @@ def test_gpt_layernorm_fold_is_bit_identical(gpu_model, seeded_sd, monkeypatch, 
 def test_fused_basicblock_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
     """Layer 1 of both trunks (stride-1 64-channel BasicBlocks) runs as one launch per block (basicblock.hip: conv1's
     output for the 18 x 18 pixels conv2 reads kept in LDS): the stage outputs, the GPT tokens pooled from the last
-    block and the whole forward are bit-identical to the two conv_x6 launches per block (DDMI_BB_FUSE=0) - the same
-    products, K order and epilogue expressions, the intermediate split as conv_x6 splits its halo."""
+    block and the whole forward are bit-identical to the two conv_x6 launches per block (the default; DDMI_BB_FUSE=1
+    enables the fused form) - the same products, K order and epilogue expressions, the intermediate split as conv_x6
+    splits its halo."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
     B = 3
@@ -601,14 +602,14 @@ def test_fused_basicblock_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
 
     gpu_model.set_gemm_mode("f16x3")
     try:
-        fused, n_fused = run(gpu_model)
-        replay = {k: v.cpu().numpy() for k, v in gpu_model.forward(feats, noise=nz, modes=True).items()}
+        ref, n_ref = run(gpu_model)
     finally:
         gpu_model.set_gemm_mode("fp32")
-    monkeypatch.setenv("DDMI_BB_FUSE", "0")
+    monkeypatch.setenv("DDMI_BB_FUSE", "1")
     m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
     try:
-        ref, n_ref = run(m)
+        fused, n_fused = run(m)
+        replay = {k: v.cpu().numpy() for k, v in m.forward(feats, noise=nz, modes=True).items()}
     finally:
         m.close()
     assert n_fused == 6 and n_ref == 0, (n_fused, n_ref)
