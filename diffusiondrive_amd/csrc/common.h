@@ -330,6 +330,8 @@ struct VprojArgs {
   int umax = 1 << 30;  // union size above which a tile falls back (tests: DDMI_VPROJ_UMAX; the kernel's capacity rules)
   unsigned* fb = nullptr;
   int fb_only = 0;     // (set by launch_vproj) the gathered kernel computes only the flagged (tile, half) pairs
+  int usplit = 1;      // union form: K split over the 16 channel groups (1, 2, 4, 8, 16); partials in `part`
+  unsigned* ucnt = nullptr;  // union form with usplit > 1: [tiles][2] arrival counters, zero between launches
 };
 bool vproj_supported(int C, int Cout, int H, int W);
 size_t vproj_tiles(int B, int cap);

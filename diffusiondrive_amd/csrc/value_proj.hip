@@ -481,9 +481,12 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  // ---- tile: the two 128-channel halves of row tile mt take blocks with equal blockIdx % 8 (one XCD)
-  const int gq = blockIdx.x / 16, rq = blockIdx.x % 16;
+  // ---- tile: the two 128-channel halves of row tile mt take blocks with equal (blockIdx / S) % 8 (one XCD); split sp
+  // of S takes channel groups [16 sp / S, 16 (sp + 1) / S)
+  const int S = a.usplit, sp = blockIdx.x % S, bq = blockIdx.x / S;
+  const int gq = bq / 16, rq = bq % 16;
   const int nh = rq / 8, mt = gq * 8 + rq % 8;
+  const int gbeg = sp * (VU_NG / S), gend = gbeg + VU_NG / S;
   rowcount_prefix(a.counts, a.B, g_pre);
   const int total = g_pre[a.B];
   const int tiles = (total + VU_BM - 1) / VU_BM;
@@ -510,7 +513,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   const int kbase = g_key[0] - 65;
   const int range = g_key[nrow - 1] + 66 - kbase;
   if (range > VU_RBITS) {
-    if (tid == 0) a.fb[mt * 2 + nh] = 1u;  // the gathered kernel computes this tile
+    if (tid == 0 && sp == 0) a.fb[mt * 2 + nh] = 1u;  // the gathered kernel computes this tile
     return;
   }
   const int nwords = (range + 31) >> 5;
@@ -555,7 +558,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   __syncthreads();
   const int U = g_usize;
   if (U > VU_UMAX || U > a.umax) {
-    if (tid == 0) a.fb[mt * 2 + nh] = 1u;
+    if (tid == 0 && sp == 0) a.fb[mt * 2 + nh] = 1u;
     return;
   }
   for (int w = tid; w < nwords; w += VU_NT) {
@@ -576,7 +579,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   // Offsets come from the slot table in LDS at each issue; the LDS write addresses are recomputed at the store.
   vu_f4 hr[VU_ALD];
   auto union_issue = [&](int g) {
-    const bool gv = g < VU_NG;
+    const bool gv = g < gend;
 #pragma unroll
     for (int i = 0; i < VU_ALD; ++i) {
       const int e = tid + VU_NT * i, u = e >> 2;
@@ -620,7 +623,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   const bool bimg_lo = (wave * VU_BPS) / VU_BQ == 1;
   const vp_i4 rwb = vp_rsrc(bimg_lo ? (const void*)a.wl : (const void*)a.wh);
   auto b_issue = [&](int slot, int tap, int g) {
-    const bool gv = g < VU_NG;
+    const bool gv = g < gend;
     const uint32_t kb = (uint32_t)(tap * kC + g * 16) * 2u;
 #pragma unroll
     for (int j = 0; j < VU_BPS; ++j) {
@@ -722,15 +725,15 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     if constexpr (t == VU_TA) union_issue(g + 1);
   };
 
-  // ---- prologue: union of group 0 -> buffer 0, B of steps 0 .. D-1, open step 0, its fragments
-  union_issue(0);
+  // ---- prologue: union of the first group -> its buffer, B of its steps 0 .. D-1, open step 0, its fragments
+  union_issue(gbeg);
 #pragma unroll
-  for (int u = 0; u < VU_D; ++u) b_issue(u % VU_NSLOT, u, 0);
+  for (int u = 0; u < VU_D; ++u) b_issue(u % VU_NSLOT, u, gbeg);
   vu_wait_vm<VU_D * VU_BPS>();
   union_tie();
-  union_store(0);
-  open_step(0, std::integral_constant<int, 0>(), std::true_type());
-  load_frag(F0, 0, 0, std::integral_constant<int, 0>());
+  union_store(gbeg & 1);
+  open_step(gbeg, std::integral_constant<int, 0>(), std::true_type());
+  load_frag(F0, 0, gbeg, std::integral_constant<int, 0>());
 
   // step s = (g, t), software pipelined: [open step s+1] [its fragment reads into the other set] [MFMAs of step s];
   // at t == TS the next group's union (loaded since the open of tap TA) goes to the other buffer, whose last reads
@@ -741,7 +744,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     constexpr int t1 = (t + 1) % 9;
     const int g1 = t == 8 ? g + 1 : g;
     if (++slot == VU_NSLOT) slot = 0;
-    if (g1 < VU_NG) {
+    if (g1 < gend) {
       open_step(g1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>());
       load_frag(Fn, slot, g1, std::integral_constant<int, t1>());
     }
@@ -768,16 +771,17 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     step(g, std::integral_constant<int, 7>(), FIRST, Bf, A);
     step(g, std::integral_constant<int, 8>(), FIRST, A, Bf);
   };
-  static_assert(VU_NG % 2 == 0, "group pairs");
-  group(0, std::true_type(), F0, F1);
-  group(1, std::false_type(), F1, F0);
-  for (int g = 2; g < VU_NG; g += 2) {
+  group(gbeg, std::true_type(), F0, F1);
+  if (gbeg + 1 < gend) group(gbeg + 1, std::false_type(), F1, F0);
+  for (int g = gbeg + 2; g < gend; g += 2) {
     group(g, std::false_type(), F0, F1);
     group(g + 1, std::false_type(), F1, F0);
   }
   vu_step_barrier<0>();  // drain the trailing (all-OOB) DMAs and LDS reads
 
-  // ---- epilogue from the accumulators: scale, bias, ReLU, the value rows out
+  // ---- epilogue from the accumulators: scale, bias, ReLU, the value rows out. With S splits each stores its scaled
+  // partial write-through, adds to the (tile, half) counter, and the last to arrive sums the partials in split order
+  // (its own from registers: deterministic whichever arrives last), as vproj_kernel<4>
   bool bad = false;
   float sc[VU_TN], bias[VU_TN];
 #pragma unroll
@@ -786,18 +790,76 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     sc[j] = a.wsinv[col];
     bias[j] = a.bias[col];
   }
+  auto row_of = [&](int i, int r) { return (wm * VU_TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh; };
 #pragma unroll
   for (int i = 0; i < VU_TM; ++i)
 #pragma unroll
     for (int j = 0; j < VU_TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = (wm * VU_TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const int ri = g_rows[row];
-        bad |= ri >= 0 && !__builtin_isfinite(acc[i][j][r]);
-        if (ri >= 0) a.out[(int64_t)ri * kC + n0 + (wn * VU_TN + j) * 32 + li] = fmaxf(acc[i][j][r] * sc[j] + bias[j], 0.f);
+        bad |= g_rows[row_of(i, r)] >= 0 && !__builtin_isfinite(acc[i][j][r]);
+        acc[i][j][r] *= sc[j];  // the scaled partial
       }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+  auto finish = [&](int i, int j, int r, float v) {
+    const int ri = g_rows[row_of(i, r)];
+    if (ri >= 0) a.out[(int64_t)ri * kC + n0 + (wn * VU_TN + j) * 32 + li] = fmaxf(v + bias[j], 0.f);
+  };
+  if (S == 1) {
+#pragma unroll
+    for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+      for (int j = 0; j < VU_TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) finish(i, j, r, acc[i][j][r]);
+    return;
+  }
+  const int64_t MR = (int64_t)a.B * a.cap;
+  const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, (int)kOOBv, 0x00020000);
+  auto part_off = [&](int s_, int i, int j, int r) {
+    return (int)((((int64_t)s_ * MR + m0 + row_of(i, r)) * kC + n0 + (wn * VU_TN + j) * 32 + li) * 4);
+  };
+#pragma unroll
+  for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+    for (int j = 0; j < VU_TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (m0 + row_of(i, r) < total) {
+          const float v = acc[i][j][r];
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rpart, part_off(sp, i, j, r), 0, kSC1);
+        }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned* cnt = a.ucnt + mt * 2 + nh;
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g_usize = old == (unsigned)(S - 1);
+    if (old == (unsigned)(S - 1)) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!g_usize) return;
+#pragma unroll
+  for (int i = 0; i < VU_TM; ++i)
+#pragma unroll
+    for (int j = 0; j < VU_TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (m0 + row_of(i, r) >= total) continue;
+        float v = 0.f;
+        for (int s_ = 0; s_ < S; ++s_) {
+          const float p = s_ == sp ? acc[i][j][r]
+                                   : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rpart, part_off(s_, i, j, r), 0, kSC1));
+          v = s_ == 0 ? p : v + p;
+        }
+        finish(i, j, r, v);
+      }
 }
 
 bool vproj_supported(int C, int Cout, int H, int W) { return C == kC && Cout == kC && H == kHW && W == kHW; }
@@ -821,8 +883,10 @@ void launch_vproj(const VprojArgs& a, hipStream_t st) {
     // two 128-channel halves per row tile, no K split: grid in groups of 8 tiles x 2 halves
     const size_t t8 = (vproj_tiles(a.B, a.cap) + 7) / 8 * 8;
     if (a.union_stage) {
-      if (!a.fb) throw std::runtime_error("vproj: the union-staged form needs its fallback flags");
-      hipLaunchKernelGGL(vproj_union_kernel, dim3((unsigned)(t8 * 2)), dim3(VU_NT), 0, st, a);
+      if (!a.fb || (a.usplit > 1 && (!a.ucnt || !a.part)) || (a.usplit & (a.usplit - 1)) || a.usplit > VU_NG)
+        throw std::runtime_error("vproj: the union-staged form needs fallback flags, a power-of-two split <= 16 "
+                                 "and, split, its counters and partials");
+      hipLaunchKernelGGL(vproj_union_kernel, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, a);
       DD_HIP_CHECK(hipGetLastError());
       VprojArgs f = a;
       f.fb_only = 1;  // tiles whose union did not fit: the gathered form
