@@ -68,6 +68,12 @@ struct MkArgs {
   unsigned* flags = nullptr;
   const float* dim_t = nullptr;   // [16] gen_sineembed_for_position's 10000^(j/16), correctly rounded
   unsigned long long* stamps = nullptr;  // diagnostics: [B][32] shader-clock stamps per phase, or nullptr
+  // query groups per scene (1, 2, 4): G workgroups of 20 / G queries each; the scene's last arriving group runs the
+  // mode selection and the next taps' dedup (scene_cnt [B] zero between launches; next_pts [B][Q*P][2] carries the
+  // DDIM-updated next points of a step's layer 1)
+  int groups = 1;
+  unsigned* scene_cnt = nullptr;
+  float* next_pts = nullptr;
 };
 
 struct MkInitArgs {

@@ -151,7 +151,12 @@ __device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int*
   }
 }
 
+// QG queries of one scene per workgroup (G = 20 / QG workgroups per scene, group gi takes queries gi QG ..): every
+// phase is per query except the mode selection and the next taps' dedup, which the scene's last arriving group runs
+template <int QG>
 __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
+  constexpr int G = kQ / QG, QGP = QG * kP;
+  static_assert(G * QG == kQ, "query groups");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* X1 = reinterpret_cast<float*>(lds);
   float* T1 = reinterpret_cast<float*>(lds + OFF_T1);
@@ -159,8 +164,10 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   char* SB = lds + OFF_SB;
   float* SM = reinterpret_cast<float*>(lds + OFF_SMALL);
   const float* __restrict__ dim_t = a.dim_t;
-  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int row0 = b * kQ;  // first global query row of the scene
+  const int b = blockIdx.x / G, gi = blockIdx.x % G, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int q0 = gi * QG;         // first query of the group in the scene
+  const int row0 = b * kQ + q0;   // its global query row
+  const int64_t pt0 = (int64_t)b * kQP + q0 * kP;  // its first (query, point) of the scene's
   const MkLayer& L = a.L;
   // diagnostic phase stamps (a separate build, DDMI_BUILD_VARIANT=stamps: -DDDMI_MK_STAMPS, and
   // MkArgs::stamps set by DDMI_MK_STAMPS=1): shader clock after each phase barrier. Compiled out of the
@@ -179,26 +186,26 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   Ring R;
   ring_fill(R, a.layer == 0 ? a.A.pa0 : L.outp, wave, 0);  // flies under the prologue
   int4* SLOT = reinterpret_cast<int4*>(SM + S_SLOT);
-  for (int t = tid; t < kQP; t += NT) SLOT[t] = reinterpret_cast<const int4*>(a.slots)[(int64_t)b * kQP + t];
+  for (int t = tid; t < QGP; t += NT) SLOT[t] = reinterpret_cast<const int4*>(a.slots)[pt0 + t];
 
   // ================================================================ layer 0: points, embedding, anchor encoder
   if (a.layer == 0) {
-    for (int t = tid; t < kQP; t += NT) {
-      const float* im = a.imgx + ((int64_t)b * kQP + t) * 2;
+    for (int t = tid; t < QGP; t += NT) {
+      const float* im = a.imgx + (pt0 + t) * 2;
       const float cx = fminf(fmaxf(im[0], -1.f), 1.f);
       const float cy = fminf(fmaxf(im[1], -1.f), 1.f);
       const float px = denorm_x(cx), py = denorm_y(cy);
       SM[S_PTS + 2 * t] = px;
       SM[S_PTS + 2 * t + 1] = py;
-      a.pts[((int64_t)b * kQP + t) * 2] = px;
-      a.pts[((int64_t)b * kQP + t) * 2 + 1] = py;
+      a.pts[(pt0 + t) * 2] = px;
+      a.pts[(pt0 + t) * 2 + 1] = py;
     }
     __syncthreads();
     stamp(1);
     // gen_sineembed_for_position: query q, point p, slot d -> column p * 64 + d of the K = 512 operand;
     // slots 2f and 2f + 1 share the angle (sin / cos); the padding queries' rows are zero
     char* EH = SA;  // [32][HP2] hi, then [32][HP2] lo
-    for (int e = tid; e < kQ * kP * 32; e += NT) {
+    for (int e = tid; e < QG * kP * 32; e += NT) {
       const int t = e >> 5, f = e & 31;  // t = q * P + p; f = coordinate half (y: 0..15, x: 16..31) x frequency
       const int q = t >> 3, p = t & 7;
       const float u = ((f < 16) ? SM[S_PTS + 2 * t + 1] : SM[S_PTS + 2 * t]) * 6.283185307179586f;
@@ -209,39 +216,43 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
       st_split(EH, HP2, q, col, sn);
       st_split(EH, HP2, q, col + 1, cs);
     }
-    for (int e = tid; e < (32 - kQ) * 512; e += NT) st_split(EH, HP2, kQ + (e >> 9), e & 511, 0.f);
+    for (int e = tid; e < (32 - QG) * 512; e += NT) st_split(EH, HP2, QG + (e >> 9), e & 511, 0.f);
     __syncthreads();
     mk_f16 acc;
     zero_acc(acc);
     mk_gemm<32>(EH, EH + 32 * HP2 * 2, HP2, a.A.pa0, wave, 0, acc, 0, R, a.A.pa3, wave, 0);
-    mk_epi<kQ>(acc, a.A.pa0, wave, a.flags, [&](int row, int col, float v) { T1[row * FP + col] = fmaxf(v, 0.f); });
+    mk_epi<QG>(acc, a.A.pa0, wave, a.flags, [&](int row, int col, float v) { T1[row * FP + col] = fmaxf(v, 0.f); });
     __syncthreads();
     stamp(2);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int q = wave + 8 * k;
+      if (q >= QG) {  // padding rows (wave-uniform): zero operand rows, no LayerNorm
+        st_split4(SA, HP, q, lane * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+        continue;
+      }
       const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], a.A.pa2g, a.A.pa2b, lane);
-      st_split4(SA, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
+      st_split4(SA, HP, q, lane * 4, q < QG ? o : make_float4(0.f, 0.f, 0.f, 0.f));
     }
     __syncthreads();
     stamp(3);
     zero_acc(acc);
     mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, a.A.pa3, wave, 0, acc, 0, R, L.outp, wave, 0);
-    mk_epi<kQ>(acc, a.A.pa3, wave, a.flags, [&](int row, int col, float v) {
-      if (row < kQ) {
+    mk_epi<QG>(acc, a.A.pa3, wave, a.flags, [&](int row, int col, float v) {
+      if (row < QG) {
         X1[row * FP + col] = v;
         a.tfe[(int64_t)(row0 + row) * kD + col] = v;
       }
     });
   } else {
-    for (int e = tid; e < kQ * 64; e += NT) {
+    for (int e = tid; e < QG * 64; e += NT) {
       const int q = e >> 6, c4 = (e & 63) * 4;
       *reinterpret_cast<float4*>(X1 + q * FP + c4) =
           *reinterpret_cast<const float4*>(a.tfe + (int64_t)(row0 + q) * kD + c4);
     }
-    for (int t = tid; t < kQP; t += NT) {
-      SM[S_PTS + 2 * t] = a.pts[((int64_t)b * kQP + t) * 2];
-      SM[S_PTS + 2 * t + 1] = a.pts[((int64_t)b * kQP + t) * 2 + 1];
+    for (int t = tid; t < QGP; t += NT) {
+      SM[S_PTS + 2 * t] = a.pts[(pt0 + t) * 2];
+      SM[S_PTS + 2 * t + 1] = a.pts[(pt0 + t) * 2 + 1];
     }
   }
   __syncthreads();
@@ -255,7 +266,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     for (int e = tid; e < kP * kD / 4; e += NT)
       *reinterpret_cast<float4*>(AW + (e >> 6) * FP + (e & 63) * 4) = reinterpret_cast<const float4*>(L.attw_w)[e];
     __syncthreads();
-    if (tid < kQP) {
+    if (tid < QGP) {
       const int q = tid >> 3, p = tid & 7;
       const float4* xr = reinterpret_cast<const float4*>(X1 + q * FP);
       const float4* wr = reinterpret_cast<const float4*>(AW + p * FP);
@@ -271,7 +282,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
       SM[S_W8 + tid] = s0 + L.attw_b[p];
     }
     __syncthreads();
-    if (tid < kQ) {
+    if (tid < QG) {
       float* w = SM + S_W8 + tid * kP;
       float mx = -INFINITY;
       for (int p = 0; p < kP; ++p) mx = fmaxf(mx, w[p]);
@@ -289,7 +300,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // rows are the gathered value_proj rows of the scene's distinct tap pixels (slots)
   for (int q = wave; q < 32; q += 8) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q < kQ) {
+    if (q < QG) {
       int4 sl[kP];
 #pragma unroll
       for (int p = 0; p < kP; ++p) sl[p] = SLOT[q * kP + p];
@@ -335,9 +346,9 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   mk_f16 acc;
   zero_acc(acc);
   mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.outp, wave, 0, acc, 0, R, L.ag_q, wave, 0);
-  mk_epi<kQ>(acc, L.outp, wave, a.flags, [&](int row, int col, float v) {
+  mk_epi<QG>(acc, L.outp, wave, a.flags, [&](int row, int col, float v) {
     float x = 0.f;
-    if (row < kQ) {
+    if (row < QG) {
       x = v + X1[row * FP + col];
       X1[row * FP + col] = x;
     }
@@ -349,8 +360,8 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // ================================================================ cross_agent_attention (+ norm1)
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ag_q, wave, 0, acc, 0, R, L.ag_out, wave, 0);
-  mk_epi<kQ>(acc, L.ag_q, wave, a.flags, [&](int row, int col, float v) {
-    if (row < kQ) T1[row * FP + col] = v;
+  mk_epi<QG>(acc, L.ag_q, wave, a.flags, [&](int row, int col, float v) {
+    if (row < QG) T1[row * FP + col] = v;
   });
   // the scene's agent K | V rows into the two split buffers (free until the output is written; the
   // barrier retires every wave's q-projection reads of SB first)
@@ -366,7 +377,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   {
     // wave = head h, lane = (query i = lane & 31, half = lane >> 5): scores of keys half*15 .. +14
     const int h = wave, i = lane & 31, half = lane >> 5;
-    const bool live = i < kQ;
+    const bool live = i < QG;
     float qv[kHD];
 #pragma unroll
     for (int e = 0; e < kHD; e += 4) {
@@ -403,7 +414,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     const float inv = 1.f / sum;
     // [head][query][key] probabilities of the live queries, pitch 33 (conflict-free column walk); the dead
     // lanes (padding queries) read a live row and their outputs are written as zeros
-    float* pr = T1 + (h * kQ + (live ? i : kQ - 1)) * 33;
+    float* pr = T1 + (h * QG + (live ? i : QG - 1)) * 33;
     if (live) {
 #pragma unroll
       for (int jj = 0; jj < KH; ++jj) pr[half * KH + jj] = sc[jj] * inv;
@@ -436,8 +447,8 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // out_proj + residual
   zero_acc(acc);
   mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.ag_out, wave, 0, acc, 0, R, L.ffn0, wave, 0);
-  mk_epi<kQ>(acc, L.ag_out, wave, a.flags, [&](int row, int col, float v) {
-    if (row < kQ) X1[row * FP + col] = v + X1[row * FP + col];
+  mk_epi<QG>(acc, L.ag_out, wave, a.flags, [&](int row, int col, float v) {
+    if (row < QG) X1[row * FP + col] = v + X1[row * FP + col];
   });
   __syncthreads();
   stamp(14);
@@ -445,15 +456,19 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   {
     const float4 eg = reinterpret_cast<const float4*>(a.ego + (int64_t)b * kD)[lane];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // rows 20..31 compute garbage that is never stored
+    for (int k = 0; k < 4; ++k) {
       const int q = wave + 8 * k;
+      if (q >= QG) {
+        st_split4(SB, HP, q, lane * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+        continue;
+      }
       float4 v = ln256(reinterpret_cast<const float4*>(X1 + q * FP)[lane], L.n1g, L.n1b, lane);
       v.x += eg.x;
       v.y += eg.y;
       v.z += eg.z;
       v.w += eg.w;
       const float4 o = ln256(v, L.n2g, L.n2b, lane);
-      st_split4(SB, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
+      st_split4(SB, HP, q, lane * 4, q < QG ? o : make_float4(0.f, 0.f, 0.f, 0.f));
     }
   }
   __syncthreads();
@@ -465,8 +480,8 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   for (int c = 0; c < kFF / kD; ++c) {
     zero_acc(acc);
     mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.ffn0, c * 8 + wave, 0, acc, 0, R, L.ffn2, wave, c * 16);
-    mk_epi<kQ>(acc, L.ffn0, c * 8 + wave, a.flags,
-           [&](int row, int col, float v) { st_split(SA, HP, row, col - c * kD, row < kQ ? fmaxf(v, 0.f) : 0.f); });
+    mk_epi<QG>(acc, L.ffn0, c * 8 + wave, a.flags,
+           [&](int row, int col, float v) { st_split(SA, HP, row, col - c * kD, row < QG ? fmaxf(v, 0.f) : 0.f); });
     __syncthreads();
     stamp(16 + 2 * c);
     const bool more = c + 1 < kFF / kD;
@@ -475,8 +490,8 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     __syncthreads();
     stamp(17 + 2 * c);
   }
-  mk_epi<kQ>(acc2, L.ffn2, wave, a.flags, [&](int row, int col, float v) {
-    if (row < kQ) T1[row * FP + col] = v;
+  mk_epi<QG>(acc2, L.ffn2, wave, a.flags, [&](int row, int col, float v) {
+    if (row < QG) T1[row * FP + col] = v;
   });
   __syncthreads();
   stamp(24);
@@ -487,12 +502,16 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int q = wave + 8 * k;
+      if (q >= QG) {
+        st_split4(SB, HP, q, lane * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+        continue;
+      }
       float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.n3g, L.n3b, lane);
       o.x = o.x * (1.f + fs.x) + fb.x;
       o.y = o.y * (1.f + fs.y) + fb.y;
       o.z = o.z * (1.f + fs.z) + fb.z;
       o.w = o.w * (1.f + fs.w) + fb.w;
-      st_split4(SB, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
+      st_split4(SB, HP, q, lane * 4, q < QG ? o : make_float4(0.f, 0.f, 0.f, 0.f));
     }
   }
   __syncthreads();
@@ -501,31 +520,35 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   // ================================================================ task decoder: cls and reg branches
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c0, wave, 0, acc, 0, R, L.r0, wave, 0);
-  mk_epi<kQ>(acc, L.c0, wave, a.flags, [&](int row, int col, float v) {
-    if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
+  mk_epi<QG>(acc, L.c0, wave, a.flags, [&](int row, int col, float v) {
+    if (row < QG) T1[row * FP + col] = fmaxf(v, 0.f);
   });
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.r0, wave, 0, acc, 0, R, L.c3, wave, 0);
-  mk_epi<kQ>(acc, L.r0, wave, a.flags, [&](int row, int col, float v) { st_split(SA, HP, row, col, row < kQ ? fmaxf(v, 0.f) : 0.f); });
+  mk_epi<QG>(acc, L.r0, wave, a.flags, [&](int row, int col, float v) { st_split(SA, HP, row, col, row < QG ? fmaxf(v, 0.f) : 0.f); });
   __syncthreads();
   stamp(26);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int q = wave + 8 * k;
+    if (q >= QG) {
+      st_split4(SB, HP, q, lane * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+      continue;
+    }
     const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c2g, L.c2b, lane);
-    st_split4(SB, HP, q, lane * 4, q < kQ ? o : make_float4(0.f, 0.f, 0.f, 0.f));
+    st_split4(SB, HP, q, lane * 4, q < QG ? o : make_float4(0.f, 0.f, 0.f, 0.f));
   }
   __syncthreads();
   stamp(27);
   zero_acc(acc);
   mk_gemm<16>(SB, SB + SPLIT_BYTES, HP, L.c3, wave, 0, acc, 0, R, L.r2, wave, 0);
-  mk_epi<kQ>(acc, L.c3, wave, a.flags, [&](int row, int col, float v) {
-    if (row < kQ) T1[row * FP + col] = fmaxf(v, 0.f);
+  mk_epi<QG>(acc, L.c3, wave, a.flags, [&](int row, int col, float v) {
+    if (row < QG) T1[row * FP + col] = fmaxf(v, 0.f);
   });
   zero_acc(acc);
   mk_gemm<16>(SA, SA + SPLIT_BYTES, HP, L.r2, wave, 0, acc, 0, R, none, 0, 0);
-  mk_epi<kQ>(acc, L.r2, wave, a.flags, [&](int row, int col, float v) {
-    if (row < kQ) X1[row * FP + col] = fmaxf(v, 0.f);
+  mk_epi<QG>(acc, L.r2, wave, a.flags, [&](int row, int col, float v) {
+    if (row < QG) X1[row * FP + col] = fmaxf(v, 0.f);
   });
   __syncthreads();
   stamp(28);
@@ -533,11 +556,12 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   {
     const float4 w = reinterpret_cast<const float4*>(L.c6_w)[lane];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {  // queries wave, wave + 8, wave + 16 (< 20 when wave < 4)
+    for (int k = 0; k < 3; ++k) {  // queries wave, wave + 8, wave + 16
       const int q = wave + 8 * k;
+      if (q >= QG) break;
       const float4 o = ln256(reinterpret_cast<const float4*>(T1 + q * FP)[lane], L.c5g, L.c5b, lane);
       const float s = wave_sum((o.x * w.x + o.y * w.y) + (o.z * w.z + o.w * w.w));
-      if (lane == 0 && q < kQ) {
+      if (lane == 0 && q < QG) {
         const float c = s + L.c6_b[0];
         SM[S_CLS + q] = c;
         a.cls_out[row0 + q] = c;
@@ -550,7 +574,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     for (int e = tid; e < kP * 3 * kD / 4; e += NT)
       *reinterpret_cast<float4*>(RW + (e >> 6) * FP + (e & 63) * 4) = reinterpret_cast<const float4*>(L.r4_w)[e];
     __syncthreads();
-    if (tid < kQ * kP * 3) {
+    if (tid < QG * kP * 3) {
       const int q = tid / (kP * 3), o = tid - q * (kP * 3);
       const float4* xr = reinterpret_cast<const float4*>(X1 + q * FP);
       const float4* wr = reinterpret_cast<const float4*>(RW + o * FP);
@@ -568,12 +592,12 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   }
   __syncthreads();
   // reg[..., :2] += points; reg[..., 2] = tanh * pi (transfuser_model_v2.py:376-380)
-  for (int t = tid; t < kQP; t += NT) {
+  for (int t = tid; t < QGP; t += NT) {
     const float* rr = SM + S_RR + t * 3;
     const float x = rr[0] + SM[S_PTS + 2 * t];
     const float y = rr[1] + SM[S_PTS + 2 * t + 1];
     const float hd = tanhf(rr[2]) * 3.14159265358979323846f;
-    float* ro = a.reg_out + ((int64_t)b * kQP + t) * 3;
+    float* ro = a.reg_out + (pt0 + t) * 3;
     ro[0] = x;
     ro[1] = y;
     ro[2] = hd;
@@ -583,8 +607,8 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     SM[S_PN + 2 * t] = x;
     SM[S_PN + 2 * t + 1] = y;
     if (a.pts_next) {
-      a.pts_next[((int64_t)b * kQP + t) * 2] = x;
-      a.pts_next[((int64_t)b * kQP + t) * 2 + 1] = y;
+      a.pts_next[(pt0 + t) * 2] = x;
+      a.pts_next[(pt0 + t) * 2 + 1] = y;
     }
   }
   __syncthreads();
@@ -592,8 +616,8 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
 
   // ================================================================ DDIM step / mode selection / next taps
   if (a.layer == 1 && a.ddim) {
-    for (int t = tid; t < kQP; t += NT) {
-      float* im = a.imgx + ((int64_t)b * kQP + t) * 2;
+    for (int t = tid; t < QGP; t += NT) {
+      float* im = a.imgx + (pt0 + t) * 2;
       const float x0x = norm_x(SM[S_REG + 3 * t]);
       const float x0y = norm_y(SM[S_REG + 3 * t + 1]);
       const float ex = (im[0] - a.sa_t * x0x) / a.sb_t;
@@ -610,6 +634,43 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     }
     __syncthreads();
     stamp(31);
+  }
+  if constexpr (G > 1) {
+    // the scene-level tail (mode selection, the next taps' dedup) needs every group's queries: each group publishes
+    // its next points (the DDIM-updated points at a step's layer 1; pts_next holds layer 0's) and arrives at the
+    // scene's counter (every wave's stores drained and released at agent scope first); the last to arrive acquires,
+    // reads the scene's cls / reg / next points back and runs the tail, then resets the counter for the next launch
+    if (a.layer == 1 && a.ddim)
+      for (int t = tid; t < QGP; t += NT) {
+        a.next_pts[(pt0 + t) * 2] = SM[S_PN + 2 * t];
+        a.next_pts[(pt0 + t) * 2 + 1] = SM[S_PN + 2 * t + 1];
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __shared__ int last;
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(a.scene_cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == (unsigned)(G - 1);
+      if (last) __hip_atomic_store(a.scene_cnt + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const float* np = (a.layer == 1 && a.ddim) ? a.next_pts : a.pts_next;
+    for (int t = tid; t < kQP; t += NT) {
+      if (a.traj) {
+        const float* ro = a.reg_out + ((int64_t)b * kQP + t) * 3;
+        SM[S_REG + 3 * t] = __builtin_nontemporal_load(ro);
+        SM[S_REG + 3 * t + 1] = __builtin_nontemporal_load(ro + 1);
+        SM[S_REG + 3 * t + 2] = __builtin_nontemporal_load(ro + 2);
+      }
+      if (a.next_rows && np) {
+        SM[S_PN + 2 * t] = __builtin_nontemporal_load(np + ((int64_t)b * kQP + t) * 2);
+        SM[S_PN + 2 * t + 1] = __builtin_nontemporal_load(np + ((int64_t)b * kQP + t) * 2 + 1);
+      }
+    }
+    if (tid < kQ) SM[S_CLS + tid] = __builtin_nontemporal_load(a.cls_out + b * kQ + tid);
+    __syncthreads();
   }
   if (a.traj && tid == 0) {
     int best = 0;
@@ -630,7 +691,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   }
 #ifdef DDMI_MK_STAMPS
   stamp(32);
-  if (a.stamps && tid < 40) a.stamps[(int64_t)b * 40 + tid] = st_lds[tid];
+  if (a.stamps && tid < 40 && G == 1) a.stamps[(int64_t)b * 40 + tid] = st_lds[tid];
 #endif
 }
 
@@ -745,9 +806,19 @@ void launch_decoder_mk(const MkArgs& a, hipStream_t st) {
   if (a.B <= 0) return;
   if (!a.dim_t || !a.slots || !a.vrows || !a.akv || !a.ego || !a.film || !a.tfe || !a.pts || !a.imgx)
     throw std::runtime_error("decoder_mk: missing operand");
-  static std::atomic<uint64_t> attr;
-  set_max_lds_once(attr, reinterpret_cast<const void*>(decoder_mk_kernel), LDS_BYTES);
-  hipLaunchKernelGGL(decoder_mk_kernel, dim3(a.B), dim3(NT), LDS_BYTES, st, a);
+  if (a.groups != 1 && (!a.scene_cnt || (a.layer == 1 && a.ddim && !a.next_pts) || (a.next_rows && a.layer == 0 && !a.pts_next)))
+    throw std::runtime_error("decoder_mk: query groups need the scene counters and the next-point buffers");
+  static std::atomic<uint64_t> attr[3];
+  auto go = [&](auto kern, int i, int g) {
+    set_max_lds_once(attr[i], reinterpret_cast<const void*>(kern), LDS_BYTES);
+    hipLaunchKernelGGL(kern, dim3(a.B * g), dim3(NT), LDS_BYTES, st, a);
+  };
+  switch (a.groups) {
+    case 1: go(decoder_mk_kernel<20>, 0, 1); break;
+    case 2: go(decoder_mk_kernel<10>, 1, 2); break;
+    case 4: go(decoder_mk_kernel<5>, 2, 4); break;
+    default: throw std::runtime_error("decoder_mk: groups must be 1, 2 or 4");
+  }
   DD_HIP_CHECK(hipGetLastError());
 }
 

@@ -230,6 +230,7 @@ class Model {
   bool decoder_mk = true;
   bool mk_ready = false;
   bool mk_stamps = false;  // diagnostics: per-phase clock stamps of the megakernel (tap "mk_stamps_s*l*")
+  int mk_groups_env = 0;   // DDMI_MK_GROUPS (1, 2, 4): decoder_mk workgroups per scene, else chosen from B
   MkLinOff m_pa0, m_pa3;
   // f16x3: the tf decoder + the trajectory head's agent / ego hoists as one megakernel launch (tfdec_mk.hip;
   // DDMI_TFDEC_MK=0: the unfused per-op chain)
@@ -360,6 +361,11 @@ class Model {
     if (const char* e = getenv("DDMI_GPT_ATTN_X3")) gpt_attn_x3 = atoi(e) != 0;
     if (const char* e = getenv("DDMI_FUSE_POOL")) fuse_pool = atoi(e) != 0;
     if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_MK_GROUPS")) {
+      mk_groups_env = atoi(e);
+      if (mk_groups_env != 1 && mk_groups_env != 2 && mk_groups_env != 4)
+        throw std::invalid_argument("DDMI_MK_GROUPS must be 1, 2 or 4");
+    }
     if (const char* e = getenv("DDMI_MAX_CHUNK")) {
       max_chunk = atoi(e);
       if (max_chunk < 1 || max_chunk > 256) throw std::invalid_argument("DDMI_MAX_CHUNK must be in [1, 256]");
@@ -869,6 +875,12 @@ class Model {
         }
         m.flags = num_flags;
         m.dim_t = W(dim_t_off);
+        // query groups: 4 workgroups of 5 queries per scene while B x 4 fits the chip (stamps: one per scene)
+        m.groups = mk_stamps ? 1 : (mk_groups_env ? mk_groups_env : (B * 4 <= num_cus() ? 4 : (B * 2 <= num_cus() ? 2 : 1)));
+        if (m.groups > 1) {
+          m.scene_cnt = reinterpret_cast<unsigned*>(buf_zeroed("mk_scene_cnt", (size_t)B));
+          m.next_pts = buf("mk_next_pts", (size_t)R * P * 2);
+        }
         if (mk_stamps) m.stamps = reinterpret_cast<unsigned long long*>(buf("mk_stamps" + sf, (size_t)B * 80));
         // algorithmic FLOPs of the launch: the 256-wide Linears (+ the anchor encoder at layer 0) and the
         // fp32 heads, 2 x rows x sum(K x N)

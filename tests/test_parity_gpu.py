@@ -622,3 +622,33 @@ def test_fused_basicblock_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
         assert np.array_equal(fused[k].reshape(-1)[:n], ref[k].reshape(-1)[:n]), k
     for k in replay:
         assert np.array_equal(replay[k], ref[k]), k  # the captured graph as well
+
+
+@pytest.mark.gpu
+def test_decoder_query_groups_are_bit_identical(gpu_model, seeded_sd, monkeypatch):
+    """decoder_mk splits a scene's 20 modes over 4 (or 2) workgroups of 5 (10) queries (the default while B x 4 fits
+    the chip); the last group to arrive at the scene's counter runs the mode selection and the next taps' dedup.
+    Every row's arithmetic is the same as in the one-workgroup form (DDMI_MK_GROUPS=1): the outputs, the selected
+    modes and the graph replays (the counters reset themselves) are bit-identical."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 3
+    inp = synthetic_inputs(B, 61)
+    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"]).cuda()
+
+    def run(groups):
+        monkeypatch.setenv("DDMI_MK_GROUPS", groups)
+        m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+        try:
+            outs = [{k: v.cpu().numpy() for k, v in m.forward(feats, noise=nz, modes=True).items()} for _ in range(3)]
+        finally:
+            m.close()
+        return outs
+
+    ref = run("1")
+    for g in ("2", "4"):
+        outs = run(g)
+        for o in outs:
+            for k in ref[0]:
+                assert np.array_equal(o[k], ref[0][k]), (g, k)
