@@ -149,7 +149,7 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // PREC 1: bf16 (64-channel chunks; the same bytes hold channels 0-31 and 32-63 of the chunk in bf16, and
 // each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
-__global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
+__global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks, int diag) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = TH * TW;
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   // hofs: element offset of (pixel, 4q) at chunk 0, or -1 (zero fill); hwad: LDS byte offset (in a
   // halo buffer) of the hi 8 bytes (bf16: of the quad's 8 bytes), -1 = no write. Kept in registers for
   // 8-wave workgroups, recomputed per use by 4-wave ones (ALD = 11), whose register file is the limit.
-  constexpr bool HKEEP = NW == 8 && ALD <= 12;
+  constexpr bool HKEEP = NW == 8 && ALD <= 12 && !SH;
   auto hofs_of = [&](int i) {
     const int e = tid + NT * i;
     const int px = e / QP, q = e % QP;
@@ -316,6 +316,12 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // PIPE: each half-step's fragment reads are issued under the previous half-step's MFMAs (two fragment sets in
+  // registers). The two-per-CU 8-wave form (128 VGPRs) keeps one set: reads, then their MFMAs - the other three
+  // waves of its SIMD cover the LDS latency. (Every step barrier drains lgkmcnt: the compiler may sink a step's
+  // MFMAs below the barrier asm, and with them the wait on its fragment reads, while another wave's DMA for step
+  // s + D already targets that slot.)
+  constexpr bool PIPE = !(SH && NW == 8);
   // fragments of one k16 half-step: F0 = (step, s2 = 0), F1 = (step, s2 = 1)
   struct Frag {
     x6h8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -398,7 +404,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   halo_tie();
   halo_store(0);
   open_step(0, std::integral_constant<int, 0>(), std::true_type());
-  load_frag(F0, 0, 0, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+  if constexpr (PIPE) load_frag(F0, 0, 0, std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
 
   // step (c, t), software pipelined: [F1 reads] [MFMAs F0] [(t == 8) halo c+1 -> other buffer]
   // [open step s+1] [F0 reads of s+1] [MFMAs F1]: every fragment read is in flight under the
@@ -406,6 +412,23 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   auto step = [&](int c, auto TAP, auto FIRST) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
+    if constexpr (!PIPE) {
+      load_frag(F0, slot, c, TAP, std::integral_constant<int, 0>());
+      mfma_frag(F0);
+      load_frag(F0, slot, c, TAP, std::integral_constant<int, 1>());
+      mfma_frag(F0);
+      if constexpr (t == 8) {
+        wait_vm<(8 - TA) * BPS>();
+        halo_tie();
+        // every wave's fragment reads of this chunk's halo have returned
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        halo_store(0);
+      }
+      if (++slot == NSLOT) slot = 0;
+      open_step(t == 8 ? c + 1 : c, std::integral_constant<int, (t + 1) % 9>(),
+                std::integral_constant<bool, first && t != 8>());
+      return;
+    }
     load_frag(F1, slot, c, TAP, std::integral_constant<int, 1>());
     __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs they overlap
     mfma_frag(F0);
@@ -466,7 +489,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH ? 2 : 1) void conv_x6_kernel(ConvA
   constexpr int IT = BM / (NT / QN);  // pixels per thread
   // (8-wave workgroups: up to 16 quads - the fragment / halo registers are dead by now; ~1 % on the BN = 128
   // layers, same-box A/B)
-  constexpr bool EARLY = IT <= (NW == 8 ? 16 : 8);
+  constexpr bool EARLY = IT <= (NW == 8 && !SH ? 16 : 8);
   x6f4 rv[IT];
   int ooff[IT];
   auto load_res = [&]() {
@@ -620,11 +643,13 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // chunk would double the 4-wave form's staging registers)
   bool sh4 = a.prec == 0 && a.Cin <= 64;
   bool b128 = bn128;
+  bool sh8 = false;  // BN = 128 as 8-wave workgroups on 8 x 16 tiles, one halo buffer, two per CU
   // micro-benchmark override, read per dispatch: DDMI_X6_CFG = 1 forces the 4-wave BN = 64 form, 2 the 8-wave BN = 64 form
   if (const char* ce = getenv("DDMI_X6_CFG")) {
     const int cf = atoi(ce);
     if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
     if (cf == 2) { sh4 = false; b128 = false; }
+    if (cf == 3 && b128 && a.prec == 0 && !wide) sh8 = true;
   }
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   if (wide) {
@@ -634,7 +659,11 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
       if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else X6(8, 32, 64, 4, 2, 2, 3, 0);
     }
   } else {
-    if (b128) {
+    if (sh8) {
+      // 8 x 16 pixels x 128 channels: 23 KB halo + 3 x 16 KB ring (71 KB), wave tile 32 x 64 under 128 VGPRs: two
+      // workgroups per CU, four waves per SIMD, one's prologue / epilogue beside the other's K loop
+      X6(8, 16, 128, 4, 2, 2, 3, 1);
+    } else if (b128) {
       X6(16, 16, 128, 4, 2, 3, 4, 0);
     } else {
       if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else X6(16, 16, 64, 4, 2, 2, 3, 0);

@@ -217,7 +217,7 @@ class Model {
   // workgroup per CU runs its phases back to back, 39.5 us per tile against ~16 us of MFMA work)
   bool bb_fuse = false;
   int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
-  int vproj_usplit_env = 0;  // DDMI_VPROJ_USPLIT (1, 2, 4, 8, 16): the union form's K split, else chosen from B
+  int vproj_usplit_env = 0;  // DDMI_VPROJ_USPLIT (1, 2, 4, 8): the union form's K split, else chosen from B
   bool stem_nchw = true;             // see use_nchw_stem
   const float** in_tab = nullptr;    // device input table: [0] camera, [1] LiDAR of the current forward
   const char* force_class = nullptr;  // profiling class of the next launch (else the chosen kernel)
@@ -344,8 +344,8 @@ class Model {
     if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_USPLIT")) {
       vproj_usplit_env = atoi(e);
-      if (vproj_usplit_env < 1 || vproj_usplit_env > 16 || (vproj_usplit_env & (vproj_usplit_env - 1)))
-        throw std::invalid_argument("DDMI_VPROJ_USPLIT must be 1, 2, 4, 8 or 16");
+      if (vproj_usplit_env < 1 || vproj_usplit_env > 8 || (vproj_usplit_env & (vproj_usplit_env - 1)))
+        throw std::invalid_argument("DDMI_VPROJ_USPLIT must be 1, 2, 4 or 8");
     }
     DD_HIP_CHECK(hipMalloc(&in_tab, 4 * sizeof(float*)));
     // zeroed on the handle's own stream and waited for: ordered before any forward, on whichever stream it runs
@@ -750,10 +750,11 @@ class Model {
         const size_t t8 = (vproj_tiles(B, MR / B) + 7) / 8 * 8;
         v.fb = reinterpret_cast<unsigned*>(buf_zeroed("vproj_fb", 2 * t8));
         // K split over channel groups while the (tile, half) units leave CUs idle: ~330 live rows per scene
-        // (B = 64: 166 units, no split; B = 1: 4 units x 16 splits)
+        // (B = 64: 166 units, no split; B = 1: 4 units x 8 splits). At most 8: the last split to arrive reads the
+        // others' partials (S x 128 KB per unit), which at 16 costs more than the K loop it saves
         const int units = 2 * (int)((B * 330 + 255) / 256);
         int us = 1;
-        while (us < 16 && units * us * 2 <= v.max_wgs) us *= 2;
+        while (us < 8 && units * us * 2 <= v.max_wgs) us *= 2;
         if (vproj_usplit_env > 0) us = vproj_usplit_env;
         v.usplit = us;
         if (us > 1) {

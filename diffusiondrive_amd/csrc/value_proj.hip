@@ -845,21 +845,40 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   }
   __syncthreads();
   if (!g_usize) return;
+  // the sum in split order, from the partials (this split's too: its stores are behind the vmcnt wait above), over
+  // 16-B quads of the tile's rows: a thread's loads of up to 8 splits x 2 quads go out together (a split past S
+  // reads nothing: OOB offset)
+  constexpr int QR = VU_BN / 4;  // quads per row
+  typedef unsigned vu_u4 __attribute__((ext_vector_type(4)));
+  for (int e0 = tid; e0 < VU_BM * QR; e0 += 2 * VU_NT) {
+    vu_f4 x[8][2];
+    int ri[2], col[2];
 #pragma unroll
-  for (int i = 0; i < VU_TM; ++i)
+    for (int k = 0; k < 2; ++k) {
+      const int e = e0 + k * VU_NT, row = e / QR;
+      col[k] = n0 + 4 * (e % QR);
+      ri[k] = m0 + row < total ? g_rows[row] : -1;
 #pragma unroll
-    for (int j = 0; j < VU_TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (m0 + row_of(i, r) >= total) continue;
-        float v = 0.f;
-        for (int s_ = 0; s_ < S; ++s_) {
-          const float p = s_ == sp ? acc[i][j][r]
-                                   : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rpart, part_off(s_, i, j, r), 0, kSC1));
-          v = s_ == 0 ? p : v + p;
-        }
-        finish(i, j, r, v);
+      for (int s_ = 0; s_ < 8; ++s_) {
+        const int off = (int)((((int64_t)s_ * MR + m0 + row) * kC + col[k]) * 4);
+        x[s_][k] = __builtin_bit_cast(vu_f4, __builtin_amdgcn_raw_buffer_load_b128(rpart, (s_ < S && ri[k] >= 0) ? off : (int)kOOBv, 0, kSC1));
       }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (ri[k] < 0) continue;
+      vu_f4 v = x[0][k];
+#pragma unroll
+      for (int s_ = 1; s_ < 8; ++s_) v = s_ < S ? v + x[s_][k] : v;
+      const vu_f4 bq = *reinterpret_cast<const vu_f4*>(a.bias + col[k]);
+      vu_f4 o = v + bq;
+      o.x = fmaxf(o.x, 0.f);
+      o.y = fmaxf(o.y, 0.f);
+      o.z = fmaxf(o.z, 0.f);
+      o.w = fmaxf(o.w, 0.f);
+      *reinterpret_cast<vu_f4*>(a.out + (int64_t)ri[k] * kC + col[k]) = o;
+    }
+  }
 }
 
 bool vproj_supported(int C, int Cout, int H, int W) { return C == kC && Cout == kC && H == kHW && W == kHW; }
@@ -883,8 +902,8 @@ void launch_vproj(const VprojArgs& a, hipStream_t st) {
     // two 128-channel halves per row tile, no K split: grid in groups of 8 tiles x 2 halves
     const size_t t8 = (vproj_tiles(a.B, a.cap) + 7) / 8 * 8;
     if (a.union_stage) {
-      if (!a.fb || (a.usplit > 1 && (!a.ucnt || !a.part)) || (a.usplit & (a.usplit - 1)) || a.usplit > VU_NG)
-        throw std::runtime_error("vproj: the union-staged form needs fallback flags, a power-of-two split <= 16 "
+      if (!a.fb || (a.usplit > 1 && (!a.ucnt || !a.part)) || (a.usplit & (a.usplit - 1)) || a.usplit > 8)
+        throw std::runtime_error("vproj: the union-staged form needs fallback flags, a power-of-two split <= 8 "
                                  "and, split, its counters and partials");
       hipLaunchKernelGGL(vproj_union_kernel, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, a);
       DD_HIP_CHECK(hipGetLastError());

@@ -165,6 +165,31 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
     assert int(flags.item()) == 0
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [
+    (8, 64, 64, 32, 200),     # Cin = 32 (one K chunk), ragged N: the case the round-4 form failed
+    (32, 20, 36, 64, 256),    # ragged tiles in H and W, two chunks
+    (64, 32, 128, 128, 128),  # image layer2 3x3
+    (64, 16, 64, 256, 256),   # image layer3 3x3
+    (64, 16, 16, 256, 256),   # LiDAR layer3
+])
+def test_conv2d_f16x3_two_per_cu_form(gpu, monkeypatch, B, H, W, Cin, Cout):
+    """conv_x6's BN = 128 form as two 8-wave workgroups per CU on 8 x 16 tiles (one halo buffer, 128 VGPRs,
+    unpipelined fragments; DDMI_X6_CFG=3, read per dispatch) against PyTorch-CPU fp64 at the f16x3 bar."""
+    monkeypatch.setenv("DDMI_X6_CFG", "3")
+    x = rnd(B, Cin, H, W, seed=71)
+    w = rnd(Cout, Cin, 3, 3, seed=72, scale=1.0 / np.sqrt(Cin * 9))
+    b = rnd(Cout, seed=73)
+    ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), 1, 1) + (r := rnd(B, Cout, H, W, seed=74)).double())
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
+    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
+                           out.data_ptr(), Cout, 3, 3, 1, 1, 1, 0, flags.data_ptr(), None), gpu)
+    assert gpu.dd_op_last_kernel().decode() == "conv_x6<8,16,128,4,2>"
+    close(out.permute(0, 3, 1, 2), ref, 3e-5)
+    assert int(flags.item()) == 0
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p,res,route", [
     (64, 8, 32, 512, 512, 3, 1, 1, True, "conv_x6<8,32,128,4,2,bf16>"),     # image layer4
     (64, 8, 8, 512, 512, 3, 1, 1, True, "conv_x6<8,8,128,2,4,bf16>"),       # LiDAR layer4 (8 x 8 maps)

@@ -429,7 +429,7 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
     tiles, each tile as two 128-channel halves, K whole, the tile's 3 x 3-neighbourhood union staged once per
     16-channel group), the same tiles gathered per (row, tap) (DDMI_VPROJ_UNION=0), the union form with every tile /
     the larger-union tiles handed to the gathered fallback (DDMI_VPROJ_UMAX=0 / 600: bit-identical to the gathered
-    form on those tiles), the union form with its K split over the channel groups 1 / 4 / 16 ways (DDMI_VPROJ_USPLIT;
+    form on those tiles), the union form with its K split over the channel groups 1 / 4 / 8 ways (DDMI_VPROJ_USPLIT;
     16 is this batch's default: the partials summed in split order by the last split), its 256 x 256 form with the K split three / two / one ways
     (DDMI_VPROJ_N=1, DDMI_VPROJ_SPLITS; the partials summed in split order by the last split), conv_x3 over the
     compacted rows (DDMI_VALUE_SPLITK=0) and conv_x3 with one tile run per scene (+ DDMI_VALUE_COMPACT=0). The
@@ -479,6 +479,7 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
     runs["union_fb_some"] = fresh(DDMI_VPROJ_UMAX="600")
     runs["union_split1"] = fresh(DDMI_VPROJ_USPLIT="1")
     runs["union_split4"] = fresh(DDMI_VPROJ_USPLIT="4")
+    runs["union_split8"] = fresh(DDMI_VPROJ_USPLIT="8")
     runs["splitk3"] = fresh(DDMI_VPROJ_N="1")
     runs["splitk2"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="2")
     runs["splitk1"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="1")
@@ -495,7 +496,7 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
         # every tile handed to the fallback: exactly the gathered two-half form
         assert np.array_equal(runs["union_fb_all"][1][k][1][live], runs["gathered2"][1][k][1][live]), k
         for v in ("splitk3", "splitk2", "splitk1", "nhalf2", "gathered2", "union_fb_some", "union_split1",
-                  "union_split4"):
+                  "union_split4", "union_split8"):
             got = runs[v][1][k]
             assert np.array_equal(rows, got[0]), (v, k)
             r = ref[k][1][live]
@@ -504,7 +505,8 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
             assert err <= 1e-5, (v, k, err)
     assert np.array_equal(ref_out, runs["x3_per_scene"][0])
     assert np.array_equal(runs["union_fb_all"][0], runs["gathered2"][0])
-    for v in ("splitk3", "splitk2", "splitk1", "nhalf2", "gathered2", "union_fb_some", "union_split1", "union_split4"):
+    for v in ("splitk3", "splitk2", "splitk1", "nhalf2", "gathered2", "union_fb_some", "union_split1", "union_split4",
+              "union_split8"):
         l2 = waypoint_l2(runs[v][0], ref_out)
         lines.append(f"  trajectory waypoint L2 {v} vs conv_x3 {l2:.3e}")
         assert l2 <= 1e-5, (v, l2)
