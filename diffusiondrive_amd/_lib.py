@@ -99,6 +99,8 @@ _SIGS = {
                                           c_void_p, c_void_p, c_void_p]),
     "dd_op_stem_pool": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
                                        c_void_p, ctypes.c_int, c_void_p, c_void_p]),
+    "dd_op_stem_pool_nchw": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
+                                            c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "dd_op_gemm": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   ctypes.c_int, ctypes.c_int, c_void_p]),
     "dd_op_gemm_batched": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,

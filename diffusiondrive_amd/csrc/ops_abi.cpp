@@ -179,13 +179,27 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
   });
 }
 
+static int dd_op_stem_pool_impl(const float* in, int src_c, int B, int H, int W, const float* wgt, const float* bias,
+                                float* out, int prec, unsigned* flags, void* stream);
+
 int dd_op_stem_pool_x3(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out,
                        unsigned* flags, void* stream) {
   return dd_op_stem_pool(in, B, H, W, wgt, bias, out, 0, flags, stream);
 }
 
+int dd_op_stem_pool_nchw(const float* in, int B, int C, int H, int W, const float* wgt, const float* bias, float* out,
+                         int prec, unsigned* flags, void* stream) {
+  if (C < 1 || C > 3) return op_guard([&] { throw std::invalid_argument("stem_pool_nchw: C must be 1..3"); });
+  return dd_op_stem_pool_impl(in, C, B, H, W, wgt, bias, out, prec, flags, stream);
+}
+
 int dd_op_stem_pool(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out, int prec,
                     unsigned* flags, void* stream) {
+  return dd_op_stem_pool_impl(in, 0, B, H, W, wgt, bias, out, prec, flags, stream);
+}
+
+static int dd_op_stem_pool_impl(const float* in, int src_c, int B, int H, int W, const float* wgt, const float* bias,
+                                float* out, int prec, unsigned* flags, void* stream) {
   return op_guard([&] {
     if (prec != 0 && prec != 1) throw std::invalid_argument("stem_pool: prec must be 0 (f16x3) or 1 (bf16)");
     const int Cin = 4, Cout = 64, K = 7 * 7 * Cin;
@@ -221,8 +235,22 @@ int dd_op_stem_pool(const float* in, int B, int H, int W, const float* wgt, cons
     a.ldh = x.ldh;
     a.flags = flags;
     const int hp = (a.Ho + 2 - 3) / 2 + 1, wp = (a.Wo + 2 - 3) / 2 + 1;
-    if (!launch_stem_pool(a, out, hp, wp, S(stream))) throw std::invalid_argument("stem_pool: shape not supported");
-    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));  // the split images die with `ar`
+    // NCHW input of src_c channels: the kernel reads its address from a device word
+    const float** word = nullptr;
+    if (src_c) {
+      DD_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&word), sizeof(const float*)));
+      DD_HIP_CHECK(hipMemcpy(word, &in, sizeof(const float*), hipMemcpyHostToDevice));
+    }
+    bool ok = false;
+    try {
+      ok = launch_stem_pool(a, out, hp, wp, S(stream), src_c ? word : nullptr, src_c);
+      DD_HIP_CHECK(hipStreamSynchronize(S(stream)));  // the split images die with `ar`
+    } catch (...) {
+      if (word) (void)hipFree(word);
+      throw;
+    }
+    if (word) DD_HIP_CHECK(hipFree(word));
+    if (!ok) throw std::invalid_argument("stem_pool: shape not supported");
   });
 }
 

@@ -72,6 +72,20 @@ constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread pe
 constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
 constexpr int LDS_BYTES = 2 * IMG_BYTES + NMT * 32 * SOP * 4;
 
+// One input channel (the LiDAR histogram, SRC_C = 1): K = 7 kh x 8 kw = 56 real taps (kw = 7 and kh = 7 zero) in 4
+// k16 steps instead of 14 over the 4-channel pixels. A lane's 8 halves are 8 consecutive input columns of one row,
+// which start at an even column 2 lx: the patch is held as 4 copies shifted by 0, 2, 4, 6 columns, so the read for
+// stem column lx comes from copy lx & 3 at the 16-B aligned column 8 (lx >> 2). Copies 2368 B apart (= 64 mod 256):
+// the 16 lanes of a ds_read_b128 group in one stem row fall on 16 distinct 4-bank groups.
+constexpr int KS1 = 4;
+constexpr int IH1 = IH + 1;                        // + a zero row for the kh = 7 padding tap
+constexpr int IP1 = 40;                            // halves per copy row (80 B: 16-B aligned rows)
+constexpr int CB1 = 2368;                          // bytes per copy (>= IH1 * IP1 * 2)
+static_assert(IH1 * IP1 * 2 <= CB1 && CB1 % 256 == 64 && IW <= IP1, "one-channel copies");
+constexpr int IMG1_BYTES = 4 * CB1;                // the 4 copies of one fp16 image
+constexpr int ILD1 = (IH * IW + NT - 1) / NT;      // input pixels per thread per tile
+constexpr int LDS1_BYTES = 2 * IMG1_BYTES + NMT * 32 * SOP * 4;
+
 __device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
   hi = __builtin_convertvector(v, sp_h4);
   const sp_f4 r = v - __builtin_convertvector(hi, sp_f4);
@@ -90,17 +104,41 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
                                                        const float* __restrict__ bias, float alpha,
                                                        float* __restrict__ out, unsigned* flags, int tiles_x,
                                                        int tiles_y, int ntiles) {
+  constexpr bool C1 = SRC_C == 1;
+  constexpr int KSN = C1 ? KS1 : KS;
+  constexpr int IMGB = C1 ? IMG1_BYTES : IMG_BYTES;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* in_hi = lds;
-  char* in_lo = lds + IMG_BYTES;
-  float* so = reinterpret_cast<float*>(lds + 2 * IMG_BYTES);
+  char* in_lo = lds + IMGB;
+  float* so = reinterpret_cast<float*>(lds + 2 * IMGB);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, hl = lane >> 5;
   const int nt = wave & 1, mg = wave >> 1;
   const int co = nt * 32 + li;
 
-  // ---- loop-invariant B fragments of this wave's 32 channels (k = kh*28 + kw*4 + ci)
-  sp_h8 bh[KS], bl[KS];
+  // ---- loop-invariant B fragments of this wave's 32 channels (k = kh*28 + kw*4 + ci; one channel: k = kh*8 + kw)
+  sp_h8 bh[KSN], bl[KSN];
+  if constexpr (C1) {
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const int kh = 2 * s + hl;
+      _Float16 h8[8], l8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool live = kh < 7 && e < 7;
+        const int64_t o = (int64_t)co * ldh + kh * 28 + e * 4;
+        h8[e] = live ? __builtin_bit_cast(_Float16, wh[o]) : (_Float16)0.f;
+        l8[e] = (live && !PREC) ? __builtin_bit_cast(_Float16, wl[o]) : (_Float16)0.f;
+      }
+      bh[s] = (sp_h8){h8[0], h8[1], h8[2], h8[3], h8[4], h8[5], h8[6], h8[7]};
+      bl[s] = (sp_h8){l8[0], l8[1], l8[2], l8[3], l8[4], l8[5], l8[6], l8[7]};
+    }
+    // the zero row under every copy (the kh = 7 padding tap reads it against zero weights)
+    for (int i = tid; i < 8 * IP1 / 2; i += NT) {
+      const int cp = i / (IP1 / 2), w = i % (IP1 / 2);
+      *reinterpret_cast<uint32_t*>(lds + cp * CB1 + IH * IP1 * 2 + 4 * w) = 0u;
+    }
+  } else {
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int kh = s >> 1, kw0 = 4 * (s & 1) + 2 * hl;
@@ -116,6 +154,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     bh[s] = __builtin_bit_cast(sp_h8, hv);
     bl[s] = __builtin_bit_cast(sp_h8, lv);
   }
+  }
   const float scl = wsinv[co] * alpha;
   const float bia = bias ? bias[co] : 0.f;
   bool bad = false;
@@ -126,13 +165,25 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     py0 = (t2 % tiles_y) * PH;
     b = t2 / tiles_y;
   };
-  sp_f4 pre[ILD];
+  sp_f4 pre[C1 ? 1 : ILD];
+  float pre1[C1 ? ILD1 : 1];
   const float* __restrict__ img = SRC_C ? *src : in;
   const int64_t plane = (int64_t)H * W;
   auto load_patch = [&](int t) {
     int b, py0, px0;
     tile_origin(t, b, py0, px0);
     const int iy0 = 4 * py0 - 5, ix0 = 4 * px0 - 5;
+    if constexpr (C1) {
+#pragma unroll
+      for (int i = 0; i < ILD1; ++i) {
+        const int e = tid + NT * i;
+        const int r = e / IW, c = e - (e / IW) * IW;
+        const int iy = iy0 + r, ix = ix0 + c;
+        const bool ok = e < IH * IW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        pre1[i] = ok ? img[(int64_t)b * plane + (int64_t)iy * W + ix] : 0.f;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < ILD; ++i) {
       const int e = tid + NT * i;
@@ -156,6 +207,34 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     }
   };
   auto store_patch = [&]() {
+    if constexpr (C1) {
+      // column c of the patch -> column c - 2 cp of copy cp (cp = 0..3; the columns a read never reaches are left)
+#pragma unroll
+      for (int i = 0; i < ILD1; ++i) {
+        const int e = tid + NT * i;
+        if (e < IH * IW) {
+          const int r = e / IW, c = e - (e / IW) * IW;
+          _Float16 h, l;
+          if constexpr (PREC == 1) {
+            h = __builtin_bit_cast(_Float16, __builtin_bit_cast(uint16_t, (__bf16)pre1[i]));
+            l = (_Float16)0.f;
+          } else {
+            h = (_Float16)pre1[i];
+            l = (_Float16)(pre1[i] - (float)h);
+          }
+#pragma unroll
+          for (int cp = 0; cp < 4; ++cp) {
+            const int cc = c - 2 * cp;
+            if (cc >= 0) {
+              const int o = cp * CB1 + (r * IP1 + cc) * 2;
+              *reinterpret_cast<_Float16*>(in_hi + o) = h;
+              if constexpr (PREC == 0) *reinterpret_cast<_Float16*>(in_lo + o) = l;
+            }
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < ILD; ++i) {
       const int e = tid + NT * i;
@@ -188,12 +267,14 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       const int p = min(m * 32 + li, NSP - 1);
       const int ly = p / SW, lx = p - (p / SW) * SW;
       const int base = (2 * ly) * IP + 2 * lx + 2 * hl;  // input pixel of (kh 0, kw 2h)
+      // one channel: copy lx & 3, row 2 ly + hl (+ 2 s), 16-B aligned column 8 (lx >> 2)
+      const int base1 = (lx & 3) * CB1 + ((2 * ly + hl) * IP1 + 8 * (lx >> 2)) * 2;
       sp_f16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int off = (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
+      for (int s = 0; s < KSN; ++s) {
+        const int off = C1 ? base1 + s * 2 * IP1 * 2 : (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
         const sp_h8 ah = *reinterpret_cast<const sp_h8*>(in_hi + off);
         if constexpr (PREC == 1) {
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_b8, ah), __builtin_bit_cast(sp_b8, bh[s]),
@@ -279,8 +360,9 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
   static std::atomic<uint64_t> attr[2][4];
   auto go = [&](auto kern, int c) {
-    set_max_lds_once(attr[a.prec][c], reinterpret_cast<const void*>(kern), LDS_BYTES);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_BYTES, st, a.in, src, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
+    const int lds = c == 1 ? LDS1_BYTES : LDS_BYTES;
+    set_max_lds_once(attr[a.prec][c], reinterpret_cast<const void*>(kern), lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, a.in, src, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
                        (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
   };
   const int c = src ? src_c : 0;

@@ -240,6 +240,11 @@ int dd_op_stem_pool_x3(const float* in, int B, int H, int W, const float* wgt, c
 /* The same with the arithmetic chosen: prec 0 = f16x3, 1 = bf16 (one bf16 product per MAC). */
 int dd_op_stem_pool(const float* in, int B, int H, int W, const float* wgt, const float* bias, float* out, int prec,
                     unsigned* flags, void* stream);
+/* The same on the reference's NCHW feature tensor of C = 1..3 channels read in place (wgt still (64,7,7,4), the
+ * missing channels' taps unused) - the path dd_forward takes for the camera (C = 3) and the LiDAR histogram (C = 1,
+ * which runs a one-channel kernel form: 4 k16 steps instead of 14). */
+int dd_op_stem_pool_nchw(const float* in, int B, int C, int H, int W, const float* wgt, const float* bias, float* out,
+                         int prec, unsigned* flags, void* stream);
 /* C (M,N) = A (M,K) . W(N,K)^T [+ bias] [+ res (M,N)] [relu] */
 int dd_op_gemm(const float* A, int M, int K, const float* W, const float* bias, const float* res, float* C, int N,
                int relu, void* stream);

@@ -246,6 +246,27 @@ def test_stem_pool_bf16(gpu, B, H, W):
     close(out.permute(0, 3, 1, 2), ref, 1e-4)
 
 
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("B,C,H,W", [(2, 1, 256, 256), (1, 1, 40, 72), (2, 1, 37, 50), (2, 3, 64, 256), (1, 2, 37, 50)])
+def test_stem_pool_nchw(gpu, B, C, H, W, prec):
+    """The fused stem on the caller's NCHW tensor (C = 1: the LiDAR histogram's one-channel form, K = 7 x 8 taps in
+    4 k16 steps from 4 column-shifted copies of the patch; C = 2, 3: 4-channel pixels) vs PyTorch fp64 (bf16: on
+    bf16-rounded operands)."""
+    x = rnd(B, C, H, W, seed=85).abs()
+    w = rnd(64, 4, 7, 7, seed=86, scale=1.0 / np.sqrt(49 * C))
+    w[:, C:] = 0.0  # taps of the missing channels (their weights are never read on the NCHW path)
+    b = rnd(64, seed=87)
+    xr, wr = (x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double()) if prec else (x.double(), w.double())
+    ref = F.max_pool2d(F.relu(F.conv2d(xr, wr[:, :C], b.double(), 2, 3)), 3, 2, 1)
+    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    xin, win, bin_ = g(x), g(w.permute(0, 2, 3, 1)), g(b)
+    ok(gpu.dd_op_stem_pool_nchw(xin.data_ptr(), B, C, H, W, win.data_ptr(), bin_.data_ptr(), out.data_ptr(), prec,
+                                flags.data_ptr(), None), gpu)
+    close(out.permute(0, 3, 1, 2), ref, 1e-4 if prec else 3e-5)
+    assert int(flags.item()) == 0
+
+
 @pytest.mark.parametrize("scale", [2.0 ** -6, 2.0 ** -10])
 def test_conv2d_f16x3_small_activations(gpu, scale):
     """The f16x3 subnormal-lo regime: activations well below 2^-3 have a lo part below fp16's

@@ -3,7 +3,7 @@
 # tests, B = 1 latency and trace, conv micro-benchmark A/B
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_ops_gpu.py -v -m gpu -x --timeout 240 --timeout-method thread -k "value_proj_variants or two_per_cu or conv2d_f16x3_b64 or forward_matches_reference_goldens" > gpurun_out/r5e_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_ops_gpu.py -v -m gpu -x --timeout 240 --timeout-method thread -k "value_proj_variants or two_per_cu or conv2d_f16x3_b64 or forward_matches_reference_goldens or stem_pool or nchw_stem" > gpurun_out/r5e_tests.log 2>&1
 rc=$?; echo "[tests] rc=$rc"; grep -E "passed|failed|Error|max err" gpurun_out/r5e_tests.log | tail -8; grep -E "union_split|trajectory" gpurun_out/parity_report.txt | tail -12; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u tools/bench_configs.py --c1-child --c1-streams 2 --steps 20 > gpurun_out/r5e_c1.log 2>&1
 rc=$?; echo "[c1] rc=$rc"; grep C1TWO gpurun_out/r5e_c1.log; [ $rc -ne 0 ] && exit $rc
