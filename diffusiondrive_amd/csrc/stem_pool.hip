@@ -72,11 +72,14 @@ constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread pe
 constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
 constexpr int LDS_BYTES = 2 * IMG_BYTES + NMT * 32 * SOP * 4;
 
-// One input channel (the LiDAR histogram, SRC_C = 1): K = 7 kh x 8 kw = 56 real taps (kw = 7 and kh = 7 zero) in 4
+// One input channel (the LiDAR histogram, SRC_C = 1), opt-in (DDMI_STEM1=1, read per dispatch): K = 7 kh x 8 kw = 56 real taps (kw = 7 and kh = 7 zero) in 4
 // k16 steps instead of 14 over the 4-channel pixels. A lane's 8 halves are 8 consecutive input columns of one row,
 // which start at an even column 2 lx: the patch is held as 4 copies shifted by 0, 2, 4, 6 columns, so the read for
 // stem column lx comes from copy lx & 3 at the 16-B aligned column 8 (lx >> 2). Copies 2368 B apart (= 64 mod 256):
 // the 16 lanes of a ds_read_b128 group in one stem row fall on 16 distinct 4-bank groups.
+// Not the default: the same products summed in another K order move the B = 64 golden's per-mode poses of an
+// intermediate layer to 1.09e-4 against the 1e-4 bar (1.3e-5 with the 4-channel order; profiles/round4_t_stem1.txt,
+// reproduced in round 5) - the per-mode outputs amplify a rounding-level change of the LiDAR stem by ~10^3.
 constexpr int KS1 = 4;
 constexpr int IH1 = IH + 1;                        // + a zero row for the kh = 7 padding tap
 constexpr int IP1 = 40;                            // halves per copy row (80 B: 16-B aligned rows)
@@ -95,7 +98,7 @@ __device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
 // SRC_C = 0: the input is the NHWC image padded to 4 channels at `in`; SRC_C = 1..3: the reference's NCHW feature
 // tensor with SRC_C channels, whose address the kernel reads from *src (a device word the runtime sets per call
 // outside the captured graph), the missing channels zero - the same 4-channel pixels, without the transpose pass.
-template <int PREC, int SRC_C>
+template <int PREC, int SRC_C, int ONE = 0>
 __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__ in, const float* const* src, int H,
                                                        int W, int Hs, int Ws,
                                                        int Hp, int Wp, const uint16_t* __restrict__ wh,
@@ -103,8 +106,9 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
                                                        const float* __restrict__ wsinv,
                                                        const float* __restrict__ bias, float alpha,
                                                        float* __restrict__ out, unsigned* flags, int tiles_x,
-                                                       int tiles_y, int ntiles) {
-  constexpr bool C1 = SRC_C == 1;
+                                                       int tiles_y, int ntiles, int diag) {
+  static_assert(!ONE || SRC_C == 1, "the one-channel form reads a one-channel NCHW input");
+  constexpr bool C1 = ONE;
   constexpr int KSN = C1 ? KS1 : KS;
   constexpr int IMGB = C1 ? IMG1_BYTES : IMG_BYTES;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -263,7 +267,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     tile_origin(t, b, py0, px0);
     const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;
     // ---- stem GEMM: wave (nt, mg) takes M tiles mg, mg + 4, mg + 8
-    for (int m = mg; m < NMT; m += MSTEP) {
+    for (int m = mg; m < NMT && !(diag & 1); m += MSTEP) {
       const int p = min(m * 32 + li, NSP - 1);
       const int ly = p / SW, lx = p - (p / SW) * SW;
       const int base = (2 * ly) * IP + 2 * lx + 2 * hl;  // input pixel of (kh 0, kw 2h)
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     }
     __syncthreads();
     // ---- 3 x 3 / 2 max pool over the stem tile: (pooled pixel, channel quad) items
-    for (int i = tid; i < PH * PW * 16; i += NT) {
+    for (int i = tid; i < PH * PW * 16 && !(diag & 2); i += NT) {
       const int q = i & 15, pp = i >> 4;
       const int py = pp / PW, px = pp - (pp / PW) * PW;
       const int gy = py0 + py, gx = px0 + px;
@@ -358,18 +362,26 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int per_cu = NT == 512 ? 1 : 2;
   const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
-  static std::atomic<uint64_t> attr[2][4];
-  auto go = [&](auto kern, int c) {
-    const int lds = c == 1 ? LDS1_BYTES : LDS_BYTES;
-    set_max_lds_once(attr[a.prec][c], reinterpret_cast<const void*>(kern), lds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, a.in, src, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
-                       (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
-  };
+  // timing diagnostic, read per dispatch (graph replays do not dispatch): DDMI_STEM_DIAG bit 0 = skip the stem GEMM and
+  // its epilogue, bit 1 = skip the pool (WRONG results; tools/micro/stem_time.py)
+  const char* de = getenv("DDMI_STEM_DIAG");
+  const int diag = de ? atoi(de) : 0;
   const int c = src ? src_c : 0;
+  const char* oe = getenv("DDMI_STEM1");
+  const bool one = c == 1 && oe && atoi(oe) != 0;
+  static std::atomic<uint64_t> attr[2][5];
+  auto go = [&](auto kern, int c) {
+    const int lds = (c == 1 && one) ? LDS1_BYTES : LDS_BYTES;
+    set_max_lds_once(attr[a.prec][c == 1 && one ? 4 : c], reinterpret_cast<const void*>(kern), lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, a.in, src, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
+                       (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles, diag);
+  };
   auto pick = [&](auto PR) {
     constexpr int P = decltype(PR)::value;
     switch (c) {
-      case 1: go(stem_pool_kernel<P, 1>, 1); break;
+      case 1:
+        if (one) go(stem_pool_kernel<P, 1, 1>, 1); else go(stem_pool_kernel<P, 1, 0>, 1);
+        break;
       case 2: go(stem_pool_kernel<P, 2>, 2); break;
       case 3: go(stem_pool_kernel<P, 3>, 3); break;
       default: go(stem_pool_kernel<P, 0>, 0); break;

@@ -248,10 +248,14 @@ def test_stem_pool_bf16(gpu, B, H, W):
 
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("B,C,H,W", [(2, 1, 256, 256), (1, 1, 40, 72), (2, 1, 37, 50), (2, 3, 64, 256), (1, 2, 37, 50)])
-def test_stem_pool_nchw(gpu, B, C, H, W, prec):
-    """The fused stem on the caller's NCHW tensor (C = 1: the LiDAR histogram's one-channel form, K = 7 x 8 taps in
-    4 k16 steps from 4 column-shifted copies of the patch; C = 2, 3: 4-channel pixels) vs PyTorch fp64 (bf16: on
-    bf16-rounded operands)."""
+@pytest.mark.parametrize("one", [False, True])
+def test_stem_pool_nchw(gpu, monkeypatch, B, C, H, W, prec, one):
+    """The fused stem on the caller's NCHW tensor (C = 1..3 as 4-channel pixels; with DDMI_STEM1=1 the LiDAR
+    histogram's opt-in one-channel form, K = 7 x 8 taps in 4 k16 steps from 4 column-shifted copies of the patch) vs
+    PyTorch fp64 (bf16: on bf16-rounded operands)."""
+    if one and C != 1:
+        pytest.skip("the one-channel form takes C = 1")
+    monkeypatch.setenv("DDMI_STEM1", "1" if one else "0")
     x = rnd(B, C, H, W, seed=85).abs()
     w = rnd(64, 4, 7, 7, seed=86, scale=1.0 / np.sqrt(49 * C))
     w[:, C:] = 0.0  # taps of the missing channels (their weights are never read on the NCHW path)

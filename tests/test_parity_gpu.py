@@ -516,12 +516,9 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
 @pytest.mark.parametrize("mode", ["f16x3", "bf16"])
 def test_nchw_stem_equals_nhwc4_stem(gpu_model, seeded_sd, monkeypatch, mode):
     """The fused stems read the caller's NCHW camera / LiDAR tensors in place (through the handle's device input
-    table) instead of an NHWC4 copy made by a transpose pass first (DDMI_STEM_NCHW=0). The camera's 4-channel pixels
-    reach the same arithmetic: its pooled map is bit-identical. The one-channel LiDAR histogram takes the one-channel
-    form (the same products, summed in another K order: 4 k16 steps of 2 rows x 8 columns instead of 14 of 4 pixels x
-    4 channels), so its pooled map agrees to fp32 rounding and the trajectory within 1e-5 (f16x3; bf16 1e-4). A
-    forward whose inputs sit at new addresses replays bit-identically (the graph reads the table, not a baked
-    pointer)."""
+    table) instead of an NHWC4 copy made by a transpose pass first (DDMI_STEM_NCHW=0): the same 4-channel pixels
+    reach the same arithmetic, so the pooled stem maps and the trajectory are bit-identical - also on a forward
+    whose inputs sit at new addresses (the captured graph reads the table, not a baked pointer)."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
     B = 3
@@ -542,12 +539,9 @@ def test_nchw_stem_equals_nhwc4_stem(gpu_model, seeded_sd, monkeypatch, mode):
     ref = m.forward(feats, noise=nz)["trajectory"].cpu().numpy()
     ref_pools = [m.tap(n).cpu().numpy() for n in ("img_pool", "lid_pool")]
     m.close()
-    assert np.array_equal(a, b)
-    assert waypoint_l2(a, ref) <= (1e-5 if mode == "f16x3" else 1e-4)
-    (ip, lp), (ir, lr) = pools, ref_pools
-    assert np.array_equal(ip[: ir.size], ir[: ip.size])
-    n = min(lp.size, lr.size)
-    assert np.abs(lp[:n] - lr[:n]).max() <= 2e-6 * max(1.0, float(np.abs(lr[:n]).max()))
+    assert np.array_equal(a, ref) and np.array_equal(b, ref)
+    for p, r in zip(pools, ref_pools):
+        assert np.array_equal(p[: r.size], r[: p.size])
 
 
 @pytest.mark.parametrize("mode", ["f16x3", "bf16"])
