@@ -170,7 +170,7 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
     (32, 20, 36, 64, 256),    # ragged tiles in H and W, two chunks
     (64, 32, 128, 128, 128),  # image layer2 3x3
     (64, 16, 64, 256, 256),   # image layer3 3x3
-    (64, 16, 16, 256, 256),   # LiDAR layer3
+    (64, 32, 32, 128, 128),   # LiDAR layer2
 ])
 def test_conv2d_f16x3_two_per_cu_form(gpu, monkeypatch, B, H, W, Cin, Cout):
     """conv_x6's BN = 128 form as two 8-wave workgroups per CU on 8 x 16 tiles (one halo buffer, 128 VGPRs,
