@@ -26,8 +26,11 @@ def kclass(name):
     n = name.replace("(anonymous namespace)::", "").split("(")[0]
     n = re.sub(r"^void\s+", "", n).replace("ddmi::", "")
     # the gathered value_proj (conv_x3's GATHER = 1 instance: the decoder's cross-BEV attention contraction)
-    if re.match(r"conv_x3_kernel<(\s*\d+\s*,){6}\s*1\s*>", n) or n.startswith("vproj_kernel"):
+    # (round 5: the union-staged form; the gathered form behind it only computes the tiles whose union overflowed)
+    if re.match(r"conv_x3_kernel<(\s*\d+\s*,){6}\s*1\s*>", n) or n.startswith("vproj_union_kernel"):
         return "value_proj"
+    if n.startswith("vproj_kernel"):
+        return "value_proj_fallback"
     return re.sub(r"<.*>", "", n).replace("_kernel", "")
 
 
