@@ -62,7 +62,6 @@ constexpr int IH = 4 * PH + 7, IW = 4 * PW + 8;    // input pixels per tile (35 
 // cycles it saves)
 constexpr int IP = 50;
 constexpr int KS = 14;                             // k16 steps
-constexpr int SP_D = 3;                            // fragment reads issued this many k16 steps ahead
 constexpr int SOP = 64;                            // stem tile pitch (floats): a 16-lane ds_read_b128 group of
                                                    // the pool (quads of pixels 2k apart) then hits 64 distinct
                                                    // banks; the epilogue's 32-lane ds_write_b32 groups are
@@ -277,29 +276,19 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       sp_f16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      // the fragment reads run SP_D steps ahead of their MFMAs (issue order pinned: the compiler otherwise reads
-      // each step's fragments just before its MFMAs and waits on them, exposing the LDS latency every step)
-      auto a_off = [&](int s) { return C1 ? base1 + s * 2 * IP1 * 2 : (base + (s >> 1) * IP + 4 * (s & 1)) * 8; };
-      sp_h8 fa[KSN], fl[KSN];
-      auto rd = [&](int s) {
-        fa[s] = *reinterpret_cast<const sp_h8*>(in_hi + a_off(s));
-        if constexpr (PREC == 0) fl[s] = *reinterpret_cast<const sp_h8*>(in_lo + a_off(s));
-      };
-#pragma unroll
-      for (int s = 0; s < SP_D && s < KSN; ++s) rd(s);
 #pragma unroll
       for (int s = 0; s < KSN; ++s) {
-        if (s + SP_D < KSN) rd(s + SP_D);
-        __builtin_amdgcn_sched_barrier(0);
+        const int off = C1 ? base1 + s * 2 * IP1 * 2 : (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
+        const sp_h8 ah = *reinterpret_cast<const sp_h8*>(in_hi + off);
         if constexpr (PREC == 1) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_b8, fa[s]), __builtin_bit_cast(sp_b8, bh[s]),
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_b8, ah), __builtin_bit_cast(sp_b8, bh[s]),
                                                         acc, 0, 0, 0);
         } else {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[s], bh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[s], bl[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[s], bh[s], acc, 0, 0, 0);
+          const sp_h8 al = *reinterpret_cast<const sp_h8*>(in_lo + off);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
       // C/D layout: column (channel) li, row (pixel) (r & 3) + 8 (r >> 2) + 4 hl
 #pragma unroll
