@@ -332,6 +332,7 @@ struct VprojArgs {
   int fb_only = 0;     // (set by launch_vproj) the gathered kernel computes only the flagged (tile, half) pairs
   int usplit = 1;      // union form: K split over the 16 channel groups (1, 2, 4, 8, 16); partials in `part`
   unsigned* ucnt = nullptr;  // union form with usplit > 1: [tiles][2] arrival counters, zero between launches
+  int diag = 0;              // timing diagnostic (DDMI_VPROJ_DIAG, read per dispatch): bit 0 = union loads read nothing, bit 1 = B DMAs read nothing (WRONG results)
 };
 bool vproj_supported(int C, int Cout, int H, int W);
 size_t vproj_tiles(int B, int cap);

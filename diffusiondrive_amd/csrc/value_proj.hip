@@ -583,7 +583,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
 #pragma unroll
     for (int i = 0; i < VU_ALD; ++i) {
       const int e = tid + VU_NT * i, u = e >> 2;
-      const bool ok = gv && u < U;
+      const bool ok = gv && u < U && !(a.diag & 1);
       const int o = ok ? g_upix[u] * kC + 4 * (e & 3) + g * 16 : 0;
       hr[i] = vu_vload(rin, ok ? (uint32_t)o * 4u : kOOBv);
     }
@@ -623,7 +623,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   const bool bimg_lo = (wave * VU_BPS) / VU_BQ == 1;
   const vp_i4 rwb = vp_rsrc(bimg_lo ? (const void*)a.wl : (const void*)a.wh);
   auto b_issue = [&](int slot, int tap, int g) {
-    const bool gv = g < gend;
+    const bool gv = g < gend && !(a.diag & 2);
     const uint32_t kb = (uint32_t)(tap * kC + g * 16) * 2u;
 #pragma unroll
     for (int j = 0; j < VU_BPS; ++j) {
@@ -905,7 +905,9 @@ void launch_vproj(const VprojArgs& a, hipStream_t st) {
       if (!a.fb || (a.usplit > 1 && (!a.ucnt || !a.part)) || (a.usplit & (a.usplit - 1)) || a.usplit > 8)
         throw std::runtime_error("vproj: the union-staged form needs fallback flags, a power-of-two split <= 8 "
                                  "and, split, its counters and partials");
-      hipLaunchKernelGGL(vproj_union_kernel, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, a);
+      VprojArgs u = a;
+      if (const char* de = getenv("DDMI_VPROJ_DIAG")) u.diag = atoi(de);
+      hipLaunchKernelGGL(vproj_union_kernel, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, u);
       DD_HIP_CHECK(hipGetLastError());
       VprojArgs f = a;
       f.fb_only = 1;  // tiles whose union did not fit: the gathered form
