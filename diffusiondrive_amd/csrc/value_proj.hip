@@ -468,6 +468,21 @@ __device__ inline void vu_split4(const vu_f4 v, uint2& hi, uint2& lo) {
 }
 }  // namespace
 
+#ifdef DDMI_VU_STAMPS
+// diagnostic build only (DDMI_BUILD_VARIANT=vust, tools/micro/vu_stamps.py): per workgroup s_memtime at start / K loop
+// entry / K loop exit / end, and wave 0's cycles inside the step barriers and the union-store waits
+__device__ unsigned long long g_vu_st[8192 * 6];
+extern "C" int dd_vu_stamps_read(unsigned long long* h, int n) {
+  void* d = nullptr;  // read, then clear for the next launch
+  if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_vu_st)) != hipSuccess) return -1;
+  if (hipMemcpy(h, d, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(d, 0, (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#define VU_STAMP(k) vust[k] = __builtin_amdgcn_s_memtime()
+#else
+#define VU_STAMP(k)
+#endif
+
 __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   __shared__ __attribute__((aligned(1024))) char lds[VU_LDS];
   __shared__ int g_rows[VU_BM];   // output row (scene b's l-th pixel: b * cap + l) of each tile row, -1 = none
@@ -480,6 +495,14 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef DDMI_VU_STAMPS
+  unsigned long long vust[6] = {0, 0, 0, 0, 0, 0};
+  auto vu_flush = [&]() {
+    if (tid == 0 && blockIdx.x < 8192)
+      for (int k = 0; k < 6; ++k) g_vu_st[blockIdx.x * 6 + k] = vust[k];
+  };
+#endif
+  VU_STAMP(0);
 
   // ---- tile: the two 128-channel halves of row tile mt take blocks with equal (blockIdx / S) % 8 (one XCD); split sp
   // of S takes channel groups [16 sp / S, 16 (sp + 1) / S)
@@ -717,7 +740,13 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
     constexpr int N = (VU_D - 1) * VU_BPS + (vu_union_in_window(t, first) ? VU_ALD : 0);
+#ifdef DDMI_VU_STAMPS
+    const unsigned long long b0 = __builtin_amdgcn_s_memtime();
     vu_step_barrier<N>();
+    vust[4] += __builtin_amdgcn_s_memtime() - b0;
+#else
+    vu_step_barrier<N>();
+#endif
     constexpr int tn = (t + VU_D) % 9;
     int ns = slot + VU_D;
     if (ns >= VU_NSLOT) ns -= VU_NSLOT;
@@ -753,8 +782,15 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (t == VU_TS) {
       // the union of group g + 1 was issued when step TA opened; younger: B issued at the opens of taps TA+1 .. TS+1
+#ifdef DDMI_VU_STAMPS
+      const unsigned long long w0 = __builtin_amdgcn_s_memtime();
       vu_wait_vm<(VU_TS + 1 - VU_TA) * VU_BPS>();
       union_tie();
+      vust[5] += __builtin_amdgcn_s_memtime() - w0;
+#else
+      vu_wait_vm<(VU_TS + 1 - VU_TA) * VU_BPS>();
+      union_tie();
+#endif
       union_store((g + 1) & 1);
     }
   };
@@ -771,6 +807,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     step(g, std::integral_constant<int, 7>(), FIRST, Bf, A);
     step(g, std::integral_constant<int, 8>(), FIRST, A, Bf);
   };
+  VU_STAMP(1);
   group(gbeg, std::true_type(), F0, F1);
   if (gbeg + 1 < gend) group(gbeg + 1, std::false_type(), F1, F0);
   for (int g = gbeg + 2; g < gend; g += 2) {
@@ -778,6 +815,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     group(g + 1, std::false_type(), F1, F0);
   }
   vu_step_barrier<0>();  // drain the trailing (all-OOB) DMAs and LDS reads
+  VU_STAMP(2);
 
   // ---- epilogue from the accumulators: scale, bias, ReLU, the value rows out. With S splits each stores its scaled
   // partial write-through, adds to the (tile, half) counter, and the last to arrive sums the partials in split order
@@ -812,6 +850,10 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
       for (int j = 0; j < VU_TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) finish(i, j, r, acc[i][j][r]);
+#ifdef DDMI_VU_STAMPS
+    VU_STAMP(3);
+    vu_flush();
+#endif
     return;
   }
   const int64_t MR = (int64_t)a.B * a.cap;
