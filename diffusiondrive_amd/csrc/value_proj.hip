@@ -412,7 +412,7 @@ constexpr int VU_UMAX = 704;                           // union rows per buffer;
 constexpr int VU_UBYTES = (VU_UMAX + 1) * 64;          // one union buffer: 45120 B
 constexpr int VU_BIMG = VU_BN * 32;                    // one B image of a ring slot: 128 rows x 16 k x 2 B
 constexpr int VU_BSLOT = 2 * VU_BIMG;                  // 8 KB
-constexpr int VU_D = 3, VU_NSLOT = 4;                  // DMA lead (steps), ring slots
+constexpr int VU_D = 3, VU_NSLOT = 5;                  // DMA lead (steps), ring slots (D + 2: see BAR2)
 constexpr int VU_BQ = VU_BN / 32;                      // DMA instructions (32 rows of 32 B) per image per step
 constexpr int VU_BPS = 2 * VU_BQ / VU_NW;              // per wave per step
 constexpr int VU_ALD = ((VU_UMAX + 1) * 4 + VU_NT - 1) / VU_NT;  // union float4 loads per thread per group
@@ -423,7 +423,7 @@ constexpr int VU_NG = kC / 16;                         // channel groups
 constexpr int VU_LDS = 2 * VU_UBYTES + VU_NSLOT * VU_BSLOT;
 static_assert(VU_BPS >= 1 && (2 * VU_BQ) % VU_NW == 0 && VU_BQ % VU_BPS == 0, "B DMA split over the waves");
 static_assert(VU_NSLOT >= VU_D + 1, "ring");
-static_assert(VU_LDS <= 128 * 1024, "LDS");
+static_assert(VU_LDS <= 136 * 1024, "LDS (the other shared arrays add ~9 KB; 160 KB per workgroup)");
 
 // 16-B slot swizzle of a 64-B union row: 16 consecutive rows at one logical slot hit 16 distinct bank groups
 __device__ inline int vu_swz(int u) { return (u >> 2) & 3; }
@@ -439,6 +439,16 @@ constexpr bool vu_union_in_window(int t, bool first) {
   return false;
 }
 static_assert(VU_TA + VU_D < VU_TS, "the union loads leave every open window before their wait");
+// union loads issued at the opens [t - D + e, t - 1] (e = 1: the barrier also covers the next step's B)
+constexpr bool vu_union_in_window_e(int t, bool first, int e) {
+  for (int j = 1; j <= VU_D - e; ++j) {
+    const int u = t - j;
+    if (first && u < 0) return false;
+    if (((u % 9) + 9) % 9 == VU_TA) return true;
+  }
+  return false;
+}
+static_assert(VU_NSLOT >= VU_D + 2, "a step without a barrier may refill the slot of step s - 2");
 
 template <int N>
 __device__ inline void vu_step_barrier() {
@@ -483,6 +493,11 @@ extern "C" int dd_vu_stamps_read(unsigned long long* h, int n) {
 #define VU_STAMP(k)
 #endif
 
+// BAR2: the step barrier only at every other step of a group pair's 18-step sequence and at every group's tap 0 (the
+// union buffer it reads was stored since the last barrier): the barrier at step s waits for the B of steps s and
+// s + 1 when s + 1 has none, and a ring slot refilled at a barrier-less step s (with B(s + D)) held step
+// s + D - NSLOT <= s - 2, which every wave finished before the barrier at s - 1 (NSLOT = D + 2)
+template <bool BAR2>
 __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   __shared__ __attribute__((aligned(1024))) char lds[VU_LDS];
   __shared__ int g_rows[VU_BM];   // output row (scene b's l-th pixel: b * cap + l) of each tile row, -1 = none
@@ -736,17 +751,23 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   // wave's LDS reads and union stores retired (lgkmcnt(0)). Then B(s + D) into the slot of step s - 1 (all its reads
   // retired), and at t == TA the next group's union loads.
   int slot = 0;
-  auto open_step = [&](int g, auto TAP, auto FIRST) {
+  auto open_step = [&](int g, auto TAP, auto FIRST, auto PAR) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
-    constexpr int N = (VU_D - 1) * VU_BPS + (vu_union_in_window(t, first) ? VU_ALD : 0);
+    constexpr int par = decltype(PAR)::value;  // the group's place in its pair: step parity (t + 9 par) & 1
+    constexpr bool bar = !BAR2 || t == 0 || ((t + par) & 1) == 0;
+    constexpr bool next_bar = !BAR2 || t == 8 || ((t + 1 + par) & 1) == 0;
+    constexpr int e = next_bar ? 0 : 1;
+    constexpr int N = (VU_D - 1 - e) * VU_BPS + (vu_union_in_window_e(t, first, e) ? VU_ALD : 0);
+    if constexpr (bar) {
 #ifdef DDMI_VU_STAMPS
-    const unsigned long long b0 = __builtin_amdgcn_s_memtime();
-    vu_step_barrier<N>();
-    vust[4] += __builtin_amdgcn_s_memtime() - b0;
+      const unsigned long long b0 = __builtin_amdgcn_s_memtime();
+      vu_step_barrier<N>();
+      vust[4] += __builtin_amdgcn_s_memtime() - b0;
 #else
-    vu_step_barrier<N>();
+      vu_step_barrier<N>();
 #endif
+    }
     constexpr int tn = (t + VU_D) % 9;
     int ns = slot + VU_D;
     if (ns >= VU_NSLOT) ns -= VU_NSLOT;
@@ -761,20 +782,22 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   vu_wait_vm<VU_D * VU_BPS>();
   union_tie();
   union_store(gbeg & 1);
-  open_step(gbeg, std::integral_constant<int, 0>(), std::true_type());
+  open_step(gbeg, std::integral_constant<int, 0>(), std::true_type(), std::integral_constant<int, 0>());
   load_frag(F0, 0, gbeg, std::integral_constant<int, 0>());
 
   // step s = (g, t), software pipelined: [open step s+1] [its fragment reads into the other set] [MFMAs of step s];
   // at t == TS the next group's union (loaded since the open of tap TA) goes to the other buffer, whose last reads
   // (group g - 1) retired long before
-  auto step = [&](int g, auto TAP, auto FIRST, Frag& Fc, Frag& Fn) {
+  auto step = [&](int g, auto TAP, auto FIRST, auto PAR, Frag& Fc, Frag& Fn) {
     constexpr int t = decltype(TAP)::value;
     constexpr bool first = decltype(FIRST)::value;
+    constexpr int par = decltype(PAR)::value;
     constexpr int t1 = (t + 1) % 9;
     const int g1 = t == 8 ? g + 1 : g;
     if (++slot == VU_NSLOT) slot = 0;
     if (g1 < gend) {
-      open_step(g1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>());
+      open_step(g1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>(),
+                std::integral_constant<int, t == 8 ? 1 - par : par>());
       load_frag(Fn, slot, g1, std::integral_constant<int, t1>());
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -796,23 +819,25 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   };
   // 9 steps of a group; the fragment sets alternate per step, so a group starting from set A leaves the next
   // group's tap 0 in set Bf (9 is odd): groups run in pairs (A, Bf), (Bf, A)
-  auto group = [&](int g, auto FIRST, Frag& A, Frag& Bf) {
-    step(g, std::integral_constant<int, 0>(), FIRST, A, Bf);
-    step(g, std::integral_constant<int, 1>(), FIRST, Bf, A);
-    step(g, std::integral_constant<int, 2>(), FIRST, A, Bf);
-    step(g, std::integral_constant<int, 3>(), FIRST, Bf, A);
-    step(g, std::integral_constant<int, 4>(), FIRST, A, Bf);
-    step(g, std::integral_constant<int, 5>(), FIRST, Bf, A);
-    step(g, std::integral_constant<int, 6>(), FIRST, A, Bf);
-    step(g, std::integral_constant<int, 7>(), FIRST, Bf, A);
-    step(g, std::integral_constant<int, 8>(), FIRST, A, Bf);
+  auto group = [&](int g, auto FIRST, auto PAR, Frag& A, Frag& Bf) {
+    step(g, std::integral_constant<int, 0>(), FIRST, PAR, A, Bf);
+    step(g, std::integral_constant<int, 1>(), FIRST, PAR, Bf, A);
+    step(g, std::integral_constant<int, 2>(), FIRST, PAR, A, Bf);
+    step(g, std::integral_constant<int, 3>(), FIRST, PAR, Bf, A);
+    step(g, std::integral_constant<int, 4>(), FIRST, PAR, A, Bf);
+    step(g, std::integral_constant<int, 5>(), FIRST, PAR, Bf, A);
+    step(g, std::integral_constant<int, 6>(), FIRST, PAR, A, Bf);
+    step(g, std::integral_constant<int, 7>(), FIRST, PAR, Bf, A);
+    step(g, std::integral_constant<int, 8>(), FIRST, PAR, A, Bf);
   };
+  const std::integral_constant<int, 0> P0;
+  const std::integral_constant<int, 1> P1;
   VU_STAMP(1);
-  group(gbeg, std::true_type(), F0, F1);
-  if (gbeg + 1 < gend) group(gbeg + 1, std::false_type(), F1, F0);
+  group(gbeg, std::true_type(), P0, F0, F1);
+  if (gbeg + 1 < gend) group(gbeg + 1, std::false_type(), P1, F1, F0);
   for (int g = gbeg + 2; g < gend; g += 2) {
-    group(g, std::false_type(), F0, F1);
-    group(g + 1, std::false_type(), F1, F0);
+    group(g, std::false_type(), P0, F0, F1);
+    group(g + 1, std::false_type(), P1, F1, F0);
   }
   vu_step_barrier<0>();  // drain the trailing (all-OOB) DMAs and LDS reads
   VU_STAMP(2);
@@ -949,7 +974,12 @@ void launch_vproj(const VprojArgs& a, hipStream_t st) {
                                  "and, split, its counters and partials");
       VprojArgs u = a;
       if (const char* de = getenv("DDMI_VPROJ_DIAG")) u.diag = atoi(de);
-      hipLaunchKernelGGL(vproj_union_kernel, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, u);
+      // DDMI_VPROJ_BAR=1: a step barrier at every step (A/B of the BAR2 schedule; same arithmetic)
+      const char* be = getenv("DDMI_VPROJ_BAR");
+      if (be && atoi(be) == 1)
+        hipLaunchKernelGGL(vproj_union_kernel<false>, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, u);
+      else
+        hipLaunchKernelGGL(vproj_union_kernel<true>, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, u);
       DD_HIP_CHECK(hipGetLastError());
       VprojArgs f = a;
       f.fb_only = 1;  // tiles whose union did not fit: the gathered form

@@ -430,7 +430,8 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
     16-channel group), the same tiles gathered per (row, tap) (DDMI_VPROJ_UNION=0), the union form with every tile /
     the larger-union tiles handed to the gathered fallback (DDMI_VPROJ_UMAX=0 / 600: bit-identical to the gathered
     form on those tiles), the union form with its K split over the channel groups 1 / 4 / 8 ways (DDMI_VPROJ_USPLIT;
-    16 is this batch's default: the partials summed in split order by the last split), its 256 x 256 form with the K split three / two / one ways
+    8 is this batch's default: the partials summed in split order by the last split; a step barrier at every step,
+    DDMI_VPROJ_BAR=1, is bit-identical to the default schedule's), its 256 x 256 form with the K split three / two / one ways
     (DDMI_VPROJ_N=1, DDMI_VPROJ_SPLITS; the partials summed in split order by the last split), conv_x3 over the
     compacted rows (DDMI_VALUE_SPLITK=0) and conv_x3 with one tile run per scene (+ DDMI_VALUE_COMPACT=0). The
     conv_x3 forms evaluate every row with the same dot products in the same K order wherever its tile sits:
@@ -480,6 +481,7 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
     runs["union_split1"] = fresh(DDMI_VPROJ_USPLIT="1")
     runs["union_split4"] = fresh(DDMI_VPROJ_USPLIT="4")
     runs["union_split8"] = fresh(DDMI_VPROJ_USPLIT="8")
+    runs["union_split1_bar1"] = fresh(DDMI_VPROJ_USPLIT="1", DDMI_VPROJ_BAR="1")
     runs["splitk3"] = fresh(DDMI_VPROJ_N="1")
     runs["splitk2"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="2")
     runs["splitk1"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="1")
@@ -503,6 +505,10 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
             err = float(np.abs(got[1][live] - r).max() / max(1.0, np.abs(r).max()))
             lines.append(f"  {k} {v}: {int(live.sum())} live rows, max rel err vs conv_x3 {err:.3e}")
             assert err <= 1e-5, (v, k, err)
+    # the barrier schedule changes no arithmetic
+    assert np.array_equal(runs["union_split1"][0], runs["union_split1_bar1"][0])
+    for k in names:
+        assert np.array_equal(runs["union_split1"][1][k][1], runs["union_split1_bar1"][1][k][1]), k
     assert np.array_equal(ref_out, runs["x3_per_scene"][0])
     assert np.array_equal(runs["union_fb_all"][0], runs["gathered2"][0])
     for v in ("splitk3", "splitk2", "splitk1", "nhalf2", "gathered2", "union_fb_some", "union_split1", "union_split4",
