@@ -795,7 +795,9 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     constexpr int t1 = (t + 1) % 9;
     const int g1 = t == 8 ? g + 1 : g;
     if (++slot == VU_NSLOT) slot = 0;
-    if (g1 < gend) {
+    // (t < 8: g1 = g < gend, known at compile time - a runtime test here would merge two paths before the MFMAs,
+    // and the compiler's wait count at the merge would make them wait for the fragment reads issued just above)
+    if (t != 8 || g1 < gend) {
       open_step(g1, std::integral_constant<int, t1>(), std::integral_constant<bool, first && t != 8>(),
                 std::integral_constant<int, t == 8 ? 1 - par : par>());
       load_frag(Fn, slot, g1, std::integral_constant<int, t1>());
