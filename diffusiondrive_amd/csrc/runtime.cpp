@@ -216,6 +216,11 @@ class Model {
   // 2.37 ms per forward against 2.06 for the two conv_x6 launches per block (profiles/round5_c_bench.json: one
   // workgroup per CU runs its phases back to back, 39.5 us per tile against ~16 us of MFMA work)
   bool bb_fuse = false;
+  // layer 1 (stage 0) of each trunk runs in chunks of scenes whose output map fits this many MB (DDMI_S0_CHUNK_MB;
+  // 0 = whole batch): a chunk's maps (16 scenes of the camera's 64 x 256 x 64 = 67 MB; the LiDAR's whole B = 64 batch)
+  // stay in the memory-side cache (MALL) from one conv to the next, so the next conv's input / residual reads hit it
+  // instead of HBM; the per-pixel arithmetic is unchanged
+  int s0_chunk_mb = 72;
   int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
   int vproj_usplit_env = 0;  // DDMI_VPROJ_USPLIT (1, 2, 4, 8): the union form's K split, else chosen from B
   bool stem_nchw = true;             // see use_nchw_stem
@@ -341,6 +346,7 @@ class Model {
     if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
     if (const char* e = getenv("DDMI_LN_FOLD")) ln_fold = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BB_FUSE")) bb_fuse = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_S0_CHUNK_MB")) s0_chunk_mb = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_USPLIT")) {
       vproj_usplit_env = atoi(e);
@@ -1397,9 +1403,21 @@ class Model {
     float* tmp1 = buf(tag + "_s" + std::to_string(s) + "_t1", (size_t)B * std::max(H * Wd, Ho * Wo) * mid);
     float* tmp2 = buf(tag + "_s" + std::to_string(s) + "_t2", (size_t)B * Ho * Wo * mid);
     float* dsb = buf(tag + "_s" + std::to_string(s) + "_ds", n_out);
+    // stage 0 (stride 1: every map of the stage has the input's geometry) in chunks of scenes, each chunk through
+    // every block before the next (s0_chunk); the temporaries are reused per chunk at the same addresses
+    const int64_t img_out_bytes = (int64_t)Ho * Wo * outc * 4;
+    const int per = (int)std::max<int64_t>(1, ((int64_t)s0_chunk_mb << 20) / img_out_bytes);
+    const int chunk = (s == 0 && stride == 1 && s0_chunk_mb > 0 && B > per && !bb_fuse) ? per : B;
+    bool all_pooled = true;
     const float* cur = x;
     int ch = H, cw = Wd;
-    float* outs[2] = {bufA, bufB};
+    for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nb = std::min(chunk, B - b0);
+    const int64_t in_img = (int64_t)H * Wd * t.ch[s], out_img = (int64_t)Ho * Wo * outc;
+    cur = x + b0 * in_img;
+    ch = H;
+    cw = Wd;
+    float* outs[2] = {bufA + b0 * out_img, bufB + b0 * out_img};
     for (size_t b = 0; b < blocks.size(); ++b) {
       const Block& blk = blocks[b];
       float* y = outs[b & 1];
@@ -1407,36 +1425,40 @@ class Model {
       const int bs = b == 0 ? stride : 1;
       const int oh = (ch + 2 - 3) / bs + 1, ow = (cw + 2 - 3) / bs + 1;
       if (blk.has_ds) {
-        conv_c(blk.ds, cur, B, ch, cw, dsb, false);
+        conv_c(blk.ds, cur, nb, ch, cw, dsb, false);
         sc = dsb;
       }
       const bool last = b + 1 == blocks.size();
       auto request_pool = [&]() {  // square windows that tile the output exactly
         if (!last || !pool || oh % pool->oh || ow % pool->ow || oh / pool->oh != ow / pool->ow) return;
         pool_next = *pool;
+        pool_next.out += b0 * pool->sn;  // this chunk's scenes
         pool_next_p = oh / pool->oh;
       };
-      if (!blk.bottleneck && bb_fuse && bs == 1 && !blk.has_ds && fused_block(blk, cur, B, ch, cw, y, request_pool)) {
+      if (!blk.bottleneck && bb_fuse && bs == 1 && !blk.has_ds && fused_block(blk, cur, nb, ch, cw, y, request_pool)) {
         // conv1 + conv2 + identity in one launch (basicblock.hip): the intermediate stays in LDS
       } else if (!blk.bottleneck) {
-        conv_c(blk.c1, cur, B, ch, cw, tmp2, true);
+        conv_c(blk.c1, cur, nb, ch, cw, tmp2, true);
         request_pool();
-        conv_c(blk.c2, tmp2, B, oh, ow, y, true, sc);
+        conv_c(blk.c2, tmp2, nb, oh, ow, y, true, sc);
       } else {
-        conv_c(blk.c1, cur, B, ch, cw, tmp1, true);
-        conv_c(blk.c2, tmp1, B, ch, cw, tmp2, true);
+        conv_c(blk.c1, cur, nb, ch, cw, tmp1, true);
+        conv_c(blk.c2, tmp1, nb, ch, cw, tmp2, true);
         request_pool();
-        conv_c(blk.c3, tmp2, B, oh, ow, y, true, sc);
+        conv_c(blk.c3, tmp2, nb, oh, ow, y, true, sc);
       }
-      if (last && pool && pooled) *pooled = pool_done;
+      if (last && pool) all_pooled = all_pooled && pool_done;
       pool_next_p = 0;
       cur = y;
       ch = oh;
       cw = ow;
     }
+    }
+    if (pool && pooled) *pooled = all_pooled;
     H = ch;
     Wd = cw;
-    return const_cast<float*>(cur);
+    // the stage output: the last block's buffer, from the first scene
+    return ((blocks.size() - 1) & 1) ? bufB : bufA;
   }
 
   // GPT fusion at scale i (transfuser_backbone.py:241-362); img (B,Hi,Wi,C), lid (B,Hl,Wl,Cl) in place.

@@ -660,3 +660,37 @@ def test_decoder_query_groups_are_bit_identical(gpu_model, seeded_sd, monkeypatc
         for o in outs:
             for k in ref[0]:
                 assert np.array_equal(o[k], ref[0][k]), (g, k)
+
+
+@pytest.mark.gpu
+def test_stage_chunk_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
+    """Layer 1 of each trunk runs in chunks of scenes whose maps fit the memory-side cache (DDMI_S0_CHUNK_MB, default
+    72 MB: 16 camera scenes), every chunk through all of the stage's blocks before the next: the same convs on the
+    same pixels, so the stage outputs, the GPT tokens pooled from them and the forward are bit-identical to the
+    whole-batch stage (DDMI_S0_CHUNK_MB=0). B = 20 with 8 MB chunks: uneven chunks (2 scenes each, camera) and a
+    LiDAR stage that chunks too."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    B = 20
+    inp = synthetic_inputs(B, 67)
+    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"]).cuda()
+    taps = ("img_s0_a", "lid_s0_a", "img_s0_b", "lid_s0_b")
+
+    def run(mb):
+        monkeypatch.setenv("DDMI_S0_CHUNK_MB", mb)
+        m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+        try:
+            outs = [{k: v.cpu().numpy() for k, v in m.forward(feats, noise=nz, modes=True).items()} for _ in range(2)]
+            outs[0].update({t: m.tap(t).cpu().numpy() for t in taps})
+        finally:
+            m.close()
+        return outs
+
+    ref = run("0")
+    for mb in ("9", "72"):
+        got = run(mb)
+        for k in ref[0]:
+            assert np.array_equal(got[0][k], ref[0][k]), (mb, k)
+        for k in ref[1]:
+            assert np.array_equal(got[1][k], ref[1][k]), (mb, k)
