@@ -216,11 +216,12 @@ class Model {
   // 2.37 ms per forward against 2.06 for the two conv_x6 launches per block (profiles/round5_c_bench.json: one
   // workgroup per CU runs its phases back to back, 39.5 us per tile against ~16 us of MFMA work)
   bool bb_fuse = false;
-  // layer 1 (stage 0) of each trunk runs in chunks of scenes whose output map fits this many MB (DDMI_S0_CHUNK_MB;
-  // 0 = whole batch): a chunk's maps (16 scenes of the camera's 64 x 256 x 64 = 67 MB; the LiDAR's whole B = 64 batch)
-  // stay in the memory-side cache (MALL) from one conv to the next, so the next conv's input / residual reads hit it
-  // instead of HBM; the per-pixel arithmetic is unchanged
-  int s0_chunk_mb = 72;
+  // opt-in (DDMI_S0_CHUNK_MB, e.g. 72): layer 1 (stage 0) of each trunk in chunks of scenes whose output map fits
+  // that many MB (16 camera scenes of 64 x 256 x 64 = 67 MB), each chunk through all of the stage's blocks, so a
+  // chunk's maps could stay in the memory-side cache (MALL) from one conv to the next; same per-pixel arithmetic.
+  // Measured slower (one B = 64 forward at a time 4880 against 4953 scenes/s, conv_x6 8.35 against 8.07 ms: the
+  // quarter-size grids lose more than the cache saves; profiles/round5_ab.md), so off by default
+  int s0_chunk_mb = 0;
   int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
   int vproj_usplit_env = 0;  // DDMI_VPROJ_USPLIT (1, 2, 4, 8): the union form's K split, else chosen from B
   bool stem_nchw = true;             // see use_nchw_stem

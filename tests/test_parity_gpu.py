@@ -664,10 +664,10 @@ def test_decoder_query_groups_are_bit_identical(gpu_model, seeded_sd, monkeypatc
 
 @pytest.mark.gpu
 def test_stage_chunk_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
-    """Layer 1 of each trunk runs in chunks of scenes whose maps fit the memory-side cache (DDMI_S0_CHUNK_MB, default
+    """Layer 1 of each trunk in chunks of scenes whose maps fit the memory-side cache (opt-in DDMI_S0_CHUNK_MB, e.g.
     72 MB: 16 camera scenes), every chunk through all of the stage's blocks before the next: the same convs on the
     same pixels, so the stage outputs, the GPT tokens pooled from them and the forward are bit-identical to the
-    whole-batch stage (DDMI_S0_CHUNK_MB=0). B = 20 with 8 MB chunks: uneven chunks (2 scenes each, camera) and a
+    whole-batch stage (the default, DDMI_S0_CHUNK_MB=0). B = 20 with 8 MB chunks: uneven chunks (2 scenes each, camera) and a
     LiDAR stage that chunks too."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
