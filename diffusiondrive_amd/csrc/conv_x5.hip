@@ -71,7 +71,9 @@ __device__ inline void chunk_barrier() {
 #ifdef DDMI_X5_NOBAR  // timing diagnostic only: races by construction
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 #else
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+  // lgkmcnt(0) as well: every fragment read of the stage refilled after this barrier has returned even if the
+  // compiler moved the MFMA that consumes it (and with it the wait) below this asm
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 #endif
 }
 
