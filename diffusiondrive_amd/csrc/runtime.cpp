@@ -1413,47 +1413,47 @@ class Model {
     const float* cur = x;
     int ch = H, cw = Wd;
     for (int b0 = 0; b0 < B; b0 += chunk) {
-    const int nb = std::min(chunk, B - b0);
-    const int64_t in_img = (int64_t)H * Wd * t.ch[s], out_img = (int64_t)Ho * Wo * outc;
-    cur = x + b0 * in_img;
-    ch = H;
-    cw = Wd;
-    float* outs[2] = {bufA + b0 * out_img, bufB + b0 * out_img};
-    for (size_t b = 0; b < blocks.size(); ++b) {
-      const Block& blk = blocks[b];
-      float* y = outs[b & 1];
-      const float* sc = cur;
-      const int bs = b == 0 ? stride : 1;
-      const int oh = (ch + 2 - 3) / bs + 1, ow = (cw + 2 - 3) / bs + 1;
-      if (blk.has_ds) {
-        conv_c(blk.ds, cur, nb, ch, cw, dsb, false);
-        sc = dsb;
+      const int nb = std::min(chunk, B - b0);
+      const int64_t in_img = (int64_t)H * Wd * t.ch[s], out_img = (int64_t)Ho * Wo * outc;
+      cur = x + b0 * in_img;
+      ch = H;
+      cw = Wd;
+      float* outs[2] = {bufA + b0 * out_img, bufB + b0 * out_img};
+      for (size_t b = 0; b < blocks.size(); ++b) {
+        const Block& blk = blocks[b];
+        float* y = outs[b & 1];
+        const float* sc = cur;
+        const int bs = b == 0 ? stride : 1;
+        const int oh = (ch + 2 - 3) / bs + 1, ow = (cw + 2 - 3) / bs + 1;
+        if (blk.has_ds) {
+          conv_c(blk.ds, cur, nb, ch, cw, dsb, false);
+          sc = dsb;
+        }
+        const bool last = b + 1 == blocks.size();
+        auto request_pool = [&]() {  // square windows that tile the output exactly
+          if (!last || !pool || oh % pool->oh || ow % pool->ow || oh / pool->oh != ow / pool->ow) return;
+          pool_next = *pool;
+          pool_next.out += b0 * pool->sn;  // this chunk's scenes
+          pool_next_p = oh / pool->oh;
+        };
+        if (!blk.bottleneck && bb_fuse && bs == 1 && !blk.has_ds && fused_block(blk, cur, nb, ch, cw, y, request_pool)) {
+          // conv1 + conv2 + identity in one launch (basicblock.hip): the intermediate stays in LDS
+        } else if (!blk.bottleneck) {
+          conv_c(blk.c1, cur, nb, ch, cw, tmp2, true);
+          request_pool();
+          conv_c(blk.c2, tmp2, nb, oh, ow, y, true, sc);
+        } else {
+          conv_c(blk.c1, cur, nb, ch, cw, tmp1, true);
+          conv_c(blk.c2, tmp1, nb, ch, cw, tmp2, true);
+          request_pool();
+          conv_c(blk.c3, tmp2, nb, oh, ow, y, true, sc);
+        }
+        if (last && pool) all_pooled = all_pooled && pool_done;
+        pool_next_p = 0;
+        cur = y;
+        ch = oh;
+        cw = ow;
       }
-      const bool last = b + 1 == blocks.size();
-      auto request_pool = [&]() {  // square windows that tile the output exactly
-        if (!last || !pool || oh % pool->oh || ow % pool->ow || oh / pool->oh != ow / pool->ow) return;
-        pool_next = *pool;
-        pool_next.out += b0 * pool->sn;  // this chunk's scenes
-        pool_next_p = oh / pool->oh;
-      };
-      if (!blk.bottleneck && bb_fuse && bs == 1 && !blk.has_ds && fused_block(blk, cur, nb, ch, cw, y, request_pool)) {
-        // conv1 + conv2 + identity in one launch (basicblock.hip): the intermediate stays in LDS
-      } else if (!blk.bottleneck) {
-        conv_c(blk.c1, cur, nb, ch, cw, tmp2, true);
-        request_pool();
-        conv_c(blk.c2, tmp2, nb, oh, ow, y, true, sc);
-      } else {
-        conv_c(blk.c1, cur, nb, ch, cw, tmp1, true);
-        conv_c(blk.c2, tmp1, nb, ch, cw, tmp2, true);
-        request_pool();
-        conv_c(blk.c3, tmp2, nb, oh, ow, y, true, sc);
-      }
-      if (last && pool) all_pooled = all_pooled && pool_done;
-      pool_next_p = 0;
-      cur = y;
-      ch = oh;
-      cw = ow;
-    }
     }
     if (pool && pooled) *pooled = all_pooled;
     H = ch;
