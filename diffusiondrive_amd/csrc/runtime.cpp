@@ -215,7 +215,7 @@ class Model {
   // DDMI_BB_FUSE=1: layer-1 BasicBlocks as one launch each (fused_block, basicblock.hip). Off by default: measured
   // 2.37 ms per forward against 2.06 for the two conv_x6 launches per block (profiles/round5_c_bench.json: one
   // workgroup per CU runs its phases back to back, 39.5 us per tile against ~16 us of MFMA work)
-  bool bb_fuse = false;
+  int bb_fuse = 0;  // DDMI_BB_FUSE: 1 = both trunks, 2 = the LiDAR trunk only, 3 = the camera trunk only
   // opt-in (DDMI_S0_CHUNK_MB, e.g. 72): layer 1 (stage 0) of each trunk in chunks of scenes whose output map fits
   // that many MB (16 camera scenes of 64 x 256 x 64 = 67 MB), each chunk through all of the stage's blocks, so a
   // chunk's maps could stay in the memory-side cache (MALL) from one conv to the next; same per-pixel arithmetic.
@@ -346,7 +346,7 @@ class Model {
     if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
     if (const char* e = getenv("DDMI_LN_FOLD")) ln_fold = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_BB_FUSE")) bb_fuse = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_BB_FUSE")) bb_fuse = std::max(0, std::min(3, atoi(e)));
     if (const char* e = getenv("DDMI_S0_CHUNK_MB")) s0_chunk_mb = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_USPLIT")) {
@@ -1408,7 +1408,8 @@ class Model {
     // every block before the next (s0_chunk); the temporaries are reused per chunk at the same addresses
     const int64_t img_out_bytes = (int64_t)Ho * Wo * outc * 4;
     const int per = (int)std::max<int64_t>(1, ((int64_t)s0_chunk_mb << 20) / img_out_bytes);
-    const int chunk = (s == 0 && stride == 1 && s0_chunk_mb > 0 && B > per && !bb_fuse) ? per : B;
+    const bool bbf = bb_fuse == 1 || (bb_fuse == 2 && tag == "lid") || (bb_fuse == 3 && tag == "img");
+    const int chunk = (s == 0 && stride == 1 && s0_chunk_mb > 0 && B > per && !bbf) ? per : B;
     bool all_pooled = true;
     const float* cur = x;
     int ch = H, cw = Wd;
@@ -1436,7 +1437,7 @@ class Model {
           pool_next.out += b0 * pool->sn;  // this chunk's scenes
           pool_next_p = oh / pool->oh;
         };
-        if (!blk.bottleneck && bb_fuse && bs == 1 && !blk.has_ds && fused_block(blk, cur, nb, ch, cw, y, request_pool)) {
+        if (!blk.bottleneck && bbf && bs == 1 && !blk.has_ds && fused_block(blk, cur, nb, ch, cw, y, request_pool)) {
           // conv1 + conv2 + identity in one launch (basicblock.hip): the intermediate stays in LDS
         } else if (!blk.bottleneck) {
           conv_c(blk.c1, cur, nb, ch, cw, tmp2, true);
