@@ -652,6 +652,18 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
     if (cf == 3 && b128 && a.prec == 0 && !wide) sh8 = true;
   }
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
+  // small grids (batches of a few scenes): the routed form would run fewer than 128 workgroups, each through the
+  // whole K loop; 8 x 8 pixel tiles x 64 channels (4 waves of 32 x 32) give 4-8x the workgroups at a quarter of the
+  // work per K step. The K order (32-channel chunk, tap, k16 half) is every form's: bit-identical results.
+  // DDMI_X6_SMALL=0 keeps the routed form.
+  {
+    const int64_t wgs = b128 ? n_sp * ((a.Cout + 127) / 128) : n_sp * ((a.Cout + 63) / 64);
+    const char* se = getenv("DDMI_X6_SMALL");
+    if (wgs < 128 && !sh8 && !(se && atoi(se) == 0)) {
+      X6(8, 8, 64, 2, 2, 2, 3, 0);
+      return true;
+    }
+  }
   if (wide) {
     if (b128) {
       X6(8, 32, 128, 4, 2, 3, 4, 0);

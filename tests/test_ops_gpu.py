@@ -165,6 +165,43 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
     assert int(flags.item()) == 0
 
 
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [
+    (1, 8, 32, 512, 512),    # image layer 4 at batch 1
+    (2, 16, 64, 256, 256),   # image layer 3
+    (1, 64, 256, 64, 64),    # image layer 1
+    (1, 12, 70, 64, 100),    # ragged H, W and N
+])
+def test_conv2d_small_grid_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin, Cout, prec):
+    """conv_x6 at small batches: 8 x 8 pixel tiles x 64 channels (4 waves) instead of the routed form, whose grid
+    would have fewer than 128 workgroups. Every form walks K in the same order (32-channel chunk, tap, k16 half), so
+    the output is bit-identical to the routed form's (DDMI_X6_SMALL=0) and within the f16x3 / bf16 bar of fp64."""
+    if prec and Cin % 64:
+        pytest.skip("bf16 takes 64-channel chunks")
+    x = rnd(B, Cin, H, W, seed=75)
+    w = rnd(Cout, Cin, 3, 3, seed=76, scale=1.0 / np.sqrt(Cin * 9))
+    b = rnd(Cout, seed=77)
+    r = rnd(B, Cout, H, W, seed=78)
+    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
+
+    def run(small):
+        monkeypatch.setenv("DDMI_X6_SMALL", small)
+        out = torch.empty(B, H, W, Cout, device=DEV)
+        flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
+                               out.data_ptr(), Cout, 3, 3, 1, 1, 1, prec, flags.data_ptr(), None), gpu)
+        assert int(flags.item()) == 0
+        return out, gpu.dd_op_last_kernel().decode()
+
+    small, route = run("1")
+    routed, route0 = run("0")
+    assert route.startswith("conv_x6<8,8,64,2,2") and route0 != route, (route, route0)
+    assert torch.equal(small, routed)
+    if prec == 0:
+        ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), 1, 1) + r.double())
+        close(small.permute(0, 3, 1, 2), ref, 3e-5)
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [
     (8, 64, 64, 32, 200),     # Cin = 32 (one K chunk), ragged N: the case the round-4 form failed
     (32, 20, 36, 64, 256),    # ragged tiles in H and W, two chunks
