@@ -655,11 +655,12 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // small grids (batches of a few scenes): the routed form would run fewer than 128 workgroups, each through the
   // whole K loop; 8 x 8 pixel tiles x 64 channels (4 waves of 32 x 32) give 4-8x the workgroups at a quarter of the
   // work per K step. The K order (32-channel chunk, tap, k16 half) is every form's: bit-identical results.
-  // DDMI_X6_SMALL=0 keeps the routed form.
+  // DDMI_X6_SMALL=0 keeps the routed form, 2 forces the small-grid form (A/B).
   {
     const int64_t wgs = b128 ? n_sp * ((a.Cout + 127) / 128) : n_sp * ((a.Cout + 63) / 64);
     const char* se = getenv("DDMI_X6_SMALL");
-    if (wgs < 128 && !sh8 && !(se && atoi(se) == 0)) {
+    const int sm = se ? atoi(se) : 1;
+    if (sm == 2 || (wgs < 128 && !sh8 && sm != 0)) {
       X6(8, 8, 64, 2, 2, 2, 3, 0);
       return true;
     }
