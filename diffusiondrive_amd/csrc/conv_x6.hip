@@ -149,7 +149,7 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // PREC 1: bf16 (64-channel chunks; the same bytes hold channels 0-31 and 32-63 of the chunk in bf16, and
 // each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
-__global__ __launch_bounds__(64 * WM * WN, SH ? (WM * WN == 8 ? 4 : 2) : 1) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
+__global__ __launch_bounds__(64 * WM * WN, SH == 2 ? 3 : (SH ? (WM * WN == 8 ? 4 : 2) : 1)) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
                                                                int ntn, int nchunks, int diag) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = TH * TW;
@@ -650,6 +650,10 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
     if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
     if (cf == 2) { sh4 = false; b128 = false; }
     if (cf == 3 && b128 && a.prec == 0 && !wide) sh8 = true;
+    if (cf == 4 && sh4 && !wide) {  // 4-wave BN = 64 on 8 x 16 tiles, one halo buffer, three per CU
+      launch_x6_cfg<8, 16, 64, 4, 1, 2, 3, 2>(a, st);
+      return true;
+    }
   }
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   // small grids (batches of a few scenes): the routed form would run fewer than 128 workgroups, each through the

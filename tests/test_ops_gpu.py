@@ -165,6 +165,38 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
     assert int(flags.item()) == 0
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [
+    (8, 64, 256, 64, 64),    # image layer 1 shape (8 scenes)
+    (16, 64, 64, 64, 64),    # LiDAR layer 1 shape
+    (4, 36, 52, 32, 64),     # ragged tiles, Cin = 32 (one chunk)
+])
+def test_conv2d_three_per_cu_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin, Cout):
+    """The 4-wave BN = 64 form on 8 x 16 tiles with one halo buffer, three workgroups per CU (DDMI_X6_CFG=4, an A/B
+    of the layer-1 shapes): the same K order as the routed two-per-CU 16 x 16 form, so bit-identical outputs."""
+    x = rnd(B, Cin, H, W, seed=81)
+    w = rnd(Cout, Cin, 3, 3, seed=82, scale=1.0 / np.sqrt(Cin * 9))
+    b = rnd(Cout, seed=83)
+    r = rnd(B, Cout, H, W, seed=84)
+    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
+
+    def run(cfg):
+        if cfg:
+            monkeypatch.setenv("DDMI_X6_CFG", cfg)
+        else:
+            monkeypatch.delenv("DDMI_X6_CFG", raising=False)
+        out = torch.empty(B, H, W, Cout, device=DEV)
+        flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
+                               out.data_ptr(), Cout, 3, 3, 1, 1, 1, 0, flags.data_ptr(), None), gpu)
+        assert int(flags.item()) == 0
+        return out, gpu.dd_op_last_kernel().decode()
+
+    three, route = run("4")
+    routed, route0 = run("")
+    assert route == "conv_x6<8,16,64,4,1>" and route0 == "conv_x6<16,16,64,4,1>", (route, route0)
+    assert torch.equal(three, routed)
+
+
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [
     (1, 8, 32, 512, 512),    # image layer 4 at batch 1
