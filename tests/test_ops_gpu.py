@@ -168,7 +168,7 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [
     (8, 64, 256, 64, 64),    # image layer 1 shape (8 scenes)
     (16, 64, 64, 64, 64),    # LiDAR layer 1 shape
-    (4, 36, 52, 32, 64),     # ragged tiles, Cin = 32 (one chunk)
+    (32, 36, 52, 32, 64),    # ragged tiles, Cin = 32 (one chunk)
 ])
 def test_conv2d_three_per_cu_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin, Cout):
     """The 4-wave BN = 64 form on 8 x 16 tiles with one halo buffer, three workgroups per CU (DDMI_X6_CFG=4, an A/B
