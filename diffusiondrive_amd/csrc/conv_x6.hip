@@ -651,7 +651,6 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
   if (cf == 2) { sh4 = false; b128 = false; }
   if (cf == 3 && b128 && a.prec == 0 && !wide) sh8 = true;
-  if (cf == 4 && a.prec == 0) { sh4 = true; b128 = false; }
   const bool sh4_3 = sh4 && cf != 4;
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   // small grids (batches of a few scenes): the routed form would run fewer than 128 workgroups, each through the

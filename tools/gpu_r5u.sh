@@ -2,7 +2,7 @@
 # round 5u: layer-1 convs at three workgroups per CU by default - tests, then bench A/B against the 16 x 16 form
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_ops_gpu.py tests/test_parity_gpu.py -v -m gpu -x --timeout 240 --timeout-method thread -k "conv2d or three_per_cu or small_grid or basicblock or forward_matches_reference_goldens or stage_chunk" > gpurun_out/r5u_tests.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_ops_gpu.py tests/test_parity_gpu.py -v -m gpu -x --timeout 240 --timeout-method thread -k "three_per_cu or conv2d_f16x3_b64" > gpurun_out/r5u_tests.log 2>&1
 rc=$?; echo "[tests] rc=$rc"; grep -E "passed|failed|Error" gpurun_out/r5u_tests.log | tail -4; [ $rc -ne 0 ] && exit $rc
 for rep in 1 2; do
   for cfg in "X=0" "DDMI_X6_CFG=4"; do
