@@ -645,13 +645,13 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   bool b128 = bn128;
   bool sh8 = false;  // BN = 128 as 8-wave workgroups on 8 x 16 tiles, one halo buffer, two per CU
   // micro-benchmark override, read per dispatch: DDMI_X6_CFG = 1 forces the 4-wave BN = 64 form, 2 the 8-wave BN = 64 form,
-  // 3 the two-per-CU BN = 128 form, 4 the 16 x 16 two-per-CU BN = 64 form instead of the 8 x 16 three-per-CU one
+  // 3 the two-per-CU BN = 128 form, 4 the 8 x 16 three-per-CU BN = 64 form for the layer-1 convs
   const char* ce = getenv("DDMI_X6_CFG");
   const int cf = ce ? atoi(ce) : 0;
   if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
   if (cf == 2) { sh4 = false; b128 = false; }
   if (cf == 3 && b128 && a.prec == 0 && !wide) sh8 = true;
-  const bool sh4_3 = sh4 && cf != 4;
+  const bool sh4_3 = sh4 && cf == 4;
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   // small grids (batches of a few scenes): the routed form would run fewer than 128 workgroups, each through the
   // whole K loop; 8 x 8 pixel tiles x 64 channels (4 waves of 32 x 32) give 4-8x the workgroups at a quarter of the
@@ -680,9 +680,10 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
     } else if (b128) {
       X6(16, 16, 128, 4, 2, 3, 4, 0);
     } else if (sh4_3) {
-      // 8 x 16 pixels x 64 channels, one halo buffer: 47 KB of LDS and 167 VGPRs, three workgroups per CU (the
-      // layer-1 convs, Cin <= 64: their 18-step K loop is short against the tile's prologue / epilogue, which a
-      // third resident workgroup overlaps; image layer 1 0.297 -> 0.288 ms, LiDAR 0.072 -> 0.069, bit-identical)
+      // opt-in: 8 x 16 pixels x 64 channels, one halo buffer: 47 KB of LDS and 167 VGPRs, three workgroups per CU
+      // (the layer-1 convs, Cin <= 64: a third resident workgroup overlaps the short K loop's prologue / epilogue;
+      // image layer 1 0.297 -> 0.288 ms, LiDAR 0.072 -> 0.069, conv_x6 8.23 -> 8.15 ms per forward, bit-identical)
+      // - but 3 lanes in flight ran 0.3 % slower with it (5461-5464 against 5471-5487 scenes/s, same box)
       X6(8, 16, 64, 4, 1, 2, 3, 2);
     } else {
       if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else X6(16, 16, 64, 4, 2, 2, 3, 0);

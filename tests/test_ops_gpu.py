@@ -130,7 +130,7 @@ def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     # the batch-dependent routes the B = 64 benchmark forward takes (bench.py's workload)
     (64, 8, 32, 512, 512, 3, 1, 1, True, True, "conv_x6<8,32,128,4,2>"),     # image layer4 (256 WGs of BN 128)
     (64, 32, 128, 128, 128, 3, 1, 1, True, True, "conv_x6<16,16,128,4,2>"),  # image layer2 3x3
-    (64, 64, 256, 64, 64, 3, 1, 1, True, True, "conv_x6<8,16,64,4,1>"),      # image layer1 (4-wave, 3 WG / CU)
+    (64, 64, 256, 64, 64, 3, 1, 1, True, True, "conv_x6<16,16,64,4,1>"),     # image layer1 (4-wave, 2 WG / CU)
     (64, 64, 256, 64, 128, 3, 2, 1, True, False, "conv_x5<256,128>"),        # image layer2 entry, 3x3 / s2
     (64, 32, 128, 128, 256, 3, 2, 1, True, False, "conv_x5<256,256>"),       # image layer3 entry, 3x3 / s2
     (1, 160, 128, 512, 2048, 1, 1, 0, True, False, "conv_x5<256,256>"),      # GPT MLP-up at C = 512 (M = 20480)
@@ -171,8 +171,8 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
     (32, 36, 52, 32, 64),    # ragged tiles, Cin = 32 (one chunk)
 ])
 def test_conv2d_three_per_cu_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin, Cout):
-    """The layer-1 route: the 4-wave BN = 64 form on 8 x 16 tiles with one halo buffer, three workgroups per CU,
-    against the 16 x 16 two-per-CU form it replaced (DDMI_X6_CFG=4): the same K order, so bit-identical outputs."""
+    """The opt-in layer-1 form (DDMI_X6_CFG=4): 4 waves, BN = 64 on 8 x 16 tiles with one halo buffer, three
+    workgroups per CU, against the routed 16 x 16 two-per-CU form: the same K order, so bit-identical outputs."""
     x = rnd(B, Cin, H, W, seed=81)
     w = rnd(Cout, Cin, 3, 3, seed=82, scale=1.0 / np.sqrt(Cin * 9))
     b = rnd(Cout, seed=83)
@@ -191,8 +191,8 @@ def test_conv2d_three_per_cu_form_is_bit_identical(gpu, monkeypatch, B, H, W, Ci
         assert int(flags.item()) == 0
         return out, gpu.dd_op_last_kernel().decode()
 
-    three, route = run("")
-    routed, route0 = run("4")
+    three, route = run("4")
+    routed, route0 = run("")
     assert route == "conv_x6<8,16,64,4,1>" and route0 == "conv_x6<16,16,64,4,1>", (route, route0)
     assert torch.equal(three, routed)
 
