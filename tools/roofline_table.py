@@ -13,7 +13,7 @@ import sys
 
 HBM_PEAK = 8000.0  # GB/s
 # trace class -> PMC class (the two summaries name the gathered value_proj and a few classes differently)
-ALIAS = {"vproj": "value_proj_fallback", "vproj_union": "value_proj"}
+ALIAS = {"vproj_union": "value_proj", "value_proj": "value_proj_fallback"}  # round 5 class names
 
 
 def main():
