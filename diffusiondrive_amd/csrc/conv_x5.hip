@@ -43,7 +43,7 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
 
-constexpr int KC = 32;                 // K chunk
+constexpr int KC = 32;                 // K chunk (KCT = 16: the deep-ring form, below)
 constexpr uint32_t kOOB5 = 0x80000000u;
 
 typedef int x5i4 __attribute__((ext_vector_type(4)));
@@ -124,20 +124,32 @@ extern "C" int dd_x5_stamps_read(unsigned long long* h, int n) {
 
 // PREC 0: f16x3; PREC 1: the bf16 mode (A converted to bf16 at fragment-read time, B = the bf16 weight
 // image, one v_mfma_f32_32x32x16_bf16 per MAC; the stage's second B image is not filled).
-template <int WM, int WN, int TM, int TN, int MODE, int NS, int PREC>
+// KCT: K chunk depth. 32 = two k16 steps per chunk; 16 = the deep-ring form: half the stage bytes, so twice
+// the stages fit (256 x 256: 4 stages of 32 KB, three chunks in flight instead of one), one k16 step and one
+// barrier per chunk. The MFMA sequence (k16 order, al*bh / ah*bl / ah*bh per step) is the same: bit-identical.
+template <int WM, int WN, int TM, int TN, int MODE, int NS, int PREC, int KCT = KC>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
-  // MODE 1: Cin % 32 == 0 and KH*KW <= 32 (scalar tap walk, per-row tap masks); MODE 0: generic K.
+  // MODE 1: Cin % KCT == 0 and KH*KW <= 32 (scalar tap walk, per-row tap masks); MODE 0: generic K.
+  static_assert(KCT == 16 || KCT == 32, "K chunk");
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  constexpr int AB = BM * KC * 4;     // A stage bytes (fp32 rows of 128 B)
-  constexpr int BB = BN * KC * 2;     // one B image (fp16 rows of 64 B)
+  constexpr int ARB = KCT * 4;        // A row bytes (fp32): 128 / 64
+  constexpr int AS = KCT / 4;         // 16-B slots per A row: 8 / 4
+  constexpr int ARPI = 64 / AS;       // A rows per DMA instruction: 8 / 16
+  constexpr int ASW = 256 / ARB;      // A rows per 256-B bank row: the swizzle key is r / ASW
+  constexpr int BRB = KCT * 2;        // B row bytes per image (fp16): 64 / 32
+  constexpr int BS = KCT / 8;         // 16-B slots per B row: 4 / 2
+  constexpr int BRPI = 64 / BS;       // B rows per DMA instruction: 16 / 32
+  constexpr int BSW = 256 / BRB;      // B rows per 256-B bank row
+  constexpr int AB = BM * ARB;        // A stage bytes
+  constexpr int BB = BN * BRB;        // one B image
   constexpr int STAGE = AB + (PREC ? 1 : 2) * BB;  // bf16: one B image (so one more stage fits)
-  constexpr int A_IN = BM / 8 / NW;   // A DMA instructions per wave per chunk (8 rows x 128 B each)
-  constexpr int B_IN = BN / 16 / NW;  // B DMA instructions per wave per chunk and image (16 rows x 64 B)
-  static_assert(A_IN >= 1 && BM % (8 * NW) == 0, "A rows per wave");
-  static_assert(B_IN >= 1 && BN % (16 * NW) == 0, "B rows per wave");
+  constexpr int A_IN = BM / ARPI / NW;   // A DMA instructions per wave per chunk
+  constexpr int B_IN = BN / BRPI / NW;   // B DMA instructions per wave per chunk and image
+  static_assert(A_IN >= 1 && BM % (ARPI * NW) == 0, "A rows per wave");
+  static_assert(B_IN >= 1 && BN % (BRPI * NW) == 0, "B rows per wave");
   static_assert(NS >= 2 && NS * STAGE <= 160 * 1024, "stages");
   constexpr int DPC = A_IN + (PREC ? 1 : 2) * B_IN;  // DMA instructions per wave per chunk
   constexpr int LDS_EPI = epi_quads_lds<WM, WN, TM, TN>();
@@ -169,14 +181,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
   const int ldh = (int)a.ldh;
   const int Kp = (K + 7) & ~7;
 
-  // ---- A DMA lanes: instruction q of this wave fills rows ar0 + q*8 .. +7; lane -> (row, LDS slot)
-  const int a_rbase = wave * A_IN * 8;
+  // ---- A DMA lanes: instruction q of this wave fills rows a_rbase + q*ARPI ..; lane -> (row, LDS slot)
+  const int a_rbase = wave * A_IN * ARPI;
   int abase[A_IN], aih0[A_IN], aiw0[A_IN], akq[A_IN];
   uint32_t amask[A_IN];
 #pragma unroll
   for (int q = 0; q < A_IN; ++q) {
-    const int r = a_rbase + q * 8 + (lane >> 3);
-    akq[q] = (lane & 7) ^ ((r >> 1) & 7);  // logical 16-B slot (4 channels) this lane fetches
+    const int r = a_rbase + q * ARPI + lane / AS;
+    akq[q] = (lane % AS) ^ ((r / ASW) % AS);  // logical 16-B slot (4 channels) this lane fetches
     const int m = m0 + r;
     const bool v = m < M;
     const int mm = v ? m : 0;
@@ -199,15 +211,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
       aiw0[q] = iw0;
     }
   }
-  // ---- B DMA lanes: instruction q fills rows b_rbase + q*16 .. +15 of each image
-  const int b_rbase = wave * B_IN * 16;
+  // ---- B DMA lanes: instruction q fills rows b_rbase + q*BRPI .. of each image
+  const int b_rbase = wave * B_IN * BRPI;
   uint32_t boff[B_IN];
   bool bok[B_IN];
   int bkb[B_IN];
 #pragma unroll
   for (int q = 0; q < B_IN; ++q) {
-    const int c = b_rbase + q * 16 + (lane >> 2);
-    const int slot = (lane & 3) ^ ((c >> 2) & 3);
+    const int c = b_rbase + q * BRPI + lane / BS;
+    const int slot = (lane % BS) ^ ((c / BSW) % BS);
     const int n = n0 + c;
     bok[q] = n < a.Cout;
     bkb[q] = slot * 8;
@@ -221,10 +233,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
 #pragma unroll
       for (int q = 0; q < A_IN; ++q) {
         const bool ok = t_tap < 32 && ((amask[q] >> (t_tap & 31)) & 1u);
-        dma16(rin, __builtin_amdgcn_readfirstlane(st + (a_rbase + q * 8) * 128), ok ? (uint32_t)(abase[q] + t_off) * 4u : kOOB5);
+        dma16(rin, __builtin_amdgcn_readfirstlane(st + (a_rbase + q * ARPI) * ARB), ok ? (uint32_t)(abase[q] + t_off) * 4u : kOOB5);
       }
-      t_ci += KC;
-      t_off += KC;
+      t_ci += KCT;
+      t_off += KCT;
       if (t_ci == a.Cin) {
         t_ci = 0;
         ++t_tap;
@@ -244,15 +256,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
         const int kw = tap - kh * a.KW;
         const int ih = aih0[q] + kh, iw = aiw0[q] + kw;
         const bool ok = kk < K && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        dma16(rin, __builtin_amdgcn_readfirstlane(st + (a_rbase + q * 8) * 128),
+        dma16(rin, __builtin_amdgcn_readfirstlane(st + (a_rbase + q * ARPI) * ARB),
               ok ? (uint32_t)(abase[q] + ih * in_sh + iw * in_sw + ci) * 4u : kOOB5);
       }
     }
 #pragma unroll
     for (int q = 0; q < B_IN; ++q) {
       const uint32_t off = (bok[q] && k0 + bkb[q] < Kp) ? boff[q] + (uint32_t)k0 * 2u : kOOB5;
-      dma16(rwh, __builtin_amdgcn_readfirstlane(st + AB + (b_rbase + q * 16) * 64), off);
-      if constexpr (PREC == 0) dma16(rwl, __builtin_amdgcn_readfirstlane(st + AB + BB + (b_rbase + q * 16) * 64), off);
+      dma16(rwh, __builtin_amdgcn_readfirstlane(st + AB + (b_rbase + q * BRPI) * BRB), off);
+      if constexpr (PREC == 0) dma16(rwl, __builtin_amdgcn_readfirstlane(st + AB + BB + (b_rbase + q * BRPI) * BRB), off);
     }
   };
 
@@ -267,26 +279,27 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // fragment read offsets per k16 step s2: A fp32 logical slots 4*s2 + 2*hh, +1; B slot 2*s2 + hh
-  int a_ro[2][TM][2], b_ro[2][TN];
+  constexpr int NS2 = KCT / 16;
+  int a_ro[NS2][TM][2], b_ro[NS2][TN];
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
+  for (int s2 = 0; s2 < NS2; ++s2) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int r = (wm * TM + i) * 32 + li;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) a_ro[s2][i][u] = r * 128 + (((4 * s2 + 2 * hh + u) ^ ((r >> 1) & 7)) << 4);
+      for (int u = 0; u < 2; ++u) a_ro[s2][i][u] = r * ARB + (((4 * s2 + 2 * hh + u) ^ ((r / ASW) % AS)) << 4);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int c = (wn * TN + j) * 32 + li;
-      b_ro[s2][j] = AB + c * 64 + (((2 * s2 + hh) ^ ((c >> 2) & 3)) << 4);
+      b_ro[s2][j] = AB + c * BRB + (((2 * s2 + hh) ^ ((c / BSW) % BS)) << 4);
     }
   }
 
-  const int nk = (K + KC - 1) / KC;
+  const int nk = (K + KCT - 1) / KCT;
   // prologue: chunks 0 .. NS-2 (the MODE 1 tap walk advances in chunk order: issue order = k order)
 #pragma unroll
-  for (int u = 0; u < NS - 1; ++u) issue(u, u * KC);
+  for (int u = 0; u < NS - 1; ++u) issue(u, u * KCT);
   int cur = 0;  // stage of chunk kc
   X5_STAMP(1);
   for (int kc = 0; kc < nk; ++kc) {
@@ -295,12 +308,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
     chunk_barrier<(NS - 2) * DPC>();
     int nxt = cur + NS - 1;
     if (nxt >= NS) nxt -= NS;
-    issue(nxt, (kc + NS - 1) * KC);
+    issue(nxt, (kc + NS - 1) * KCT);
     const char* st = lds + cur * STAGE;
     if (++cur == NS) cur = 0;
     if constexpr (PREC == 1) {
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
+      for (int s2 = 0; s2 < NS2; ++s2) {
         bf16x8_t ab[TM], bb[TN];
 #pragma unroll
         for (int j = 0; j < TN; ++j) bb[j] = *reinterpret_cast<const bf16x8_t*>(st + b_ro[s2][j]);
@@ -317,7 +330,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
       continue;
     }
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    for (int s2 = 0; s2 < NS2; ++s2) {
       half8_t ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -414,29 +427,38 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M
 #endif
 }
 
-template <int WM, int WN, int TM, int TN, int NS, int PREC>
+template <int WM, int WN, int TM, int TN, int NS, int PREC, int KCT>
 static void launch_x5_one(const ConvArgs& a, int M, int K, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int ntm = (M + BM - 1) / BM;
   const int ntn = (a.Cout + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, 1);
-  static const std::string name =
-      "conv_x5<" + std::to_string(BM) + "," + std::to_string(BN) + (PREC ? ",bf16>" : ">");
+  static const std::string name = "conv_x5<" + std::to_string(BM) + "," + std::to_string(BN) +
+                                  (KCT == 16 ? ",k16" : "") + (PREC ? ",bf16>" : ">");
   set_last_conv_config(name.c_str());
-  if (a.Cin % KC == 0 && a.KH * a.KW <= 32)
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS, PREC>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
-                       ntn);
+  if (a.Cin % KCT == 0 && a.KH * a.KW <= 32)
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 1, NS, PREC, KCT>), grid, dim3(64 * WM * WN), 0, st, a, M, K,
+                       ntm, ntn);
   else
-    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS, PREC>), grid, dim3(64 * WM * WN), 0, st, a, M, K, ntm,
-                       ntn);
+    hipLaunchKernelGGL((conv_x5_kernel<WM, WN, TM, TN, 0, NS, PREC, KCT>), grid, dim3(64 * WM * WN), 0, st, a, M, K,
+                       ntm, ntn);
   DD_HIP_CHECK(hipGetLastError());
 }
-template <int WM, int WN, int TM, int TN, int NS>
+// NS: stages of the 32-deep form; the deep-ring form (DDMI_X5_DEEP, read per dispatch) runs 16-deep chunks in
+// the stages that fit the same LDS budget (NS16)
+template <int WM, int WN, int TM, int TN, int NS, int NS16 = 0>
 static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
+  if constexpr (NS16 > 0) {
+    const char* de = getenv("DDMI_X5_DEEP");
+    if (de && atoi(de) && a.prec == 0) {
+      launch_x5_one<WM, WN, TM, TN, NS16, 0, 16>(a, M, K, st);
+      return;
+    }
+  }
   if (a.prec == 1)
-    launch_x5_one<WM, WN, TM, TN, NS + 1, 1>(a, M, K, st);  // the freed B image buys a stage
+    launch_x5_one<WM, WN, TM, TN, NS + 1, 1, KC>(a, M, K, st);  // the freed B image buys a stage
   else
-    launch_x5_one<WM, WN, TM, TN, NS, 0>(a, M, K, st);
+    launch_x5_one<WM, WN, TM, TN, NS, 0, KC>(a, M, K, st);
 }
 
 // Returns false when the shape is better served by conv_x3 (grids too small to fill the chip).
@@ -477,11 +499,11 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
     if (m256 < 256) return false;
     launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st);  // 256 x 64, 4 waves
   } else if (a.Cout > 128 && m256 * n256 >= 256) {
-    launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);  // 256 x 256, 8 waves
+    launch_x5_cfg<4, 2, 2, 4, 2, 4>(a, M, K, st);  // 256 x 256, 8 waves
   } else if (a.Cout <= 128 && m256 * n128 >= 256) {
     launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);  // 256 x 128, 8 waves
   } else if (gemm && a.Cout >= 512 && a.Cout % 256 == 0 && m256 * n256 >= 128) {
-    launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);
+    launch_x5_cfg<4, 2, 2, 4, 2, 4>(a, M, K, st);
   } else if (gemm && a.Cout % 256 == 128 && m256 * n128 >= 192) {
     launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);
   } else {

@@ -234,6 +234,41 @@ def test_conv2d_small_grid_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin,
         close(small.permute(0, 3, 1, 2), ref, 3e-5)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s", [
+    (64, 320, 1, 512, 2048, 1, 1),   # GPT MLP-up at C = 512 (256 x 256 tiles)
+    (64, 320, 1, 512, 1536, 1, 1),   # GPT qkv at C = 512
+    (64, 32, 128, 128, 256, 3, 2),   # image layer-3 stride-2 3x3 (generic K walk)
+    (40, 160, 2, 520, 768, 1, 1),    # ragged K (520 = 32 x 16 + 8) and M
+])
+def test_conv_x5_deep_ring_is_bit_identical(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
+    """conv_x5's opt-in deep-ring form (DDMI_X5_DEEP=1, read per dispatch: 16-deep K chunks in 4 stages at
+    256 x 256 tiles) runs the same MFMA sequence as the 32-deep 2-stage form: bit-identical outputs."""
+    p = k // 2
+    x = rnd(B, Cin, H, W, seed=81)
+    w = rnd(Cout, Cin, k, k, seed=82, scale=1.0 / np.sqrt(Cin * k * k))
+    b = rnd(Cout, seed=83)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    r = rnd(B, Cout, Ho, Wo, seed=84)
+    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
+
+    def run(deep):
+        monkeypatch.setenv("DDMI_X5_DEEP", deep)
+        out = torch.empty(B, Ho, Wo, Cout, device=DEV)
+        flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
+                               out.data_ptr(), Cout, k, k, s, p, 1, 0, flags.data_ptr(), None), gpu)
+        assert int(flags.item()) == 0
+        return out, gpu.dd_op_last_kernel().decode()
+
+    deep, route = run("1")
+    base, route0 = run("0")
+    assert route == "conv_x5<256,256,k16>" and route0 == "conv_x5<256,256>", (route, route0)
+    assert torch.equal(deep, base)
+    if B * Ho * Wo * Cout * Cin * k * k < 6e9:  # the fp64 CPU reference only where it takes seconds
+        ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), s, p) + r.double())
+        close(deep.permute(0, 3, 1, 2), ref, 3e-5)
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [
     (8, 64, 64, 32, 200),     # Cin = 32 (one K chunk), ragged N: the case the round-4 form failed
     (32, 20, 36, 64, 256),    # ragged tiles in H and W, two chunks
