@@ -104,6 +104,7 @@ struct ConvArgs {
   const float* ln_b = nullptr;
 };
 constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
+constexpr unsigned DD_NUM_SYNC_TIMEOUT = 2u;  // a megakernel's inter-workgroup wait gave up (tfdec_mk groups)
 
 #ifdef __HIPCC__
 // Implicit-GEMM epilogue row table: element offsets of output / residual row m0 + r (r < BM) of a tile,

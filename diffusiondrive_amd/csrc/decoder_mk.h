@@ -120,6 +120,11 @@ struct TfMkArgs {
   float* akv[2] = {nullptr, nullptr};  // [B][30][512]
   float* ego[2] = {nullptr, nullptr};  // [B][256]
   int B = 0;
+  // groups = 4: four workgroups per scene (heads / hidden chunks split over them, exchanges through xbuf):
+  // xbuf [B][9][4][32][256] floats (one buffer per exchange), sync_cnt [B] zeroed by the launcher
+  int groups = 1;
+  float* xbuf = nullptr;
+  unsigned* sync_cnt = nullptr;
   unsigned* flags = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostics (stamps build): [B][40] shader-clock stamps per phase
 };

@@ -241,6 +241,7 @@ class Model {
   // f16x3: the tf decoder + the trajectory head's agent / ego hoists as one megakernel launch (tfdec_mk.hip;
   // DDMI_TFDEC_MK=0: the unfused per-op chain)
   bool tfdec_mk = true;
+  int tf_groups_env = 0;  // DDMI_TF_GROUPS=1 / 4: force the one- / four-workgroup-per-scene tf-decoder kernel
   bool gpt_attn_x3 = true;  // f16x3 GPT attention in the f16x3 / bf16 modes (DDMI_GPT_ATTN_X3=0: the fp32-MFMA kernel)
   bool fuse_pool = true;    // GPT token pooling in the stage-final conv_x6 epilogue (DDMI_FUSE_POOL=0: avgpool launches)
   bool tf_mk_ready = false;
@@ -365,6 +366,7 @@ class Model {
     }
     if (const char* e = getenv("DDMI_DECODER_MK")) decoder_mk = atoi(e) != 0;
     if (const char* e = getenv("DDMI_TFDEC_MK")) tfdec_mk = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_TF_GROUPS")) tf_groups_env = atoi(e);
     if (const char* e = getenv("DDMI_GPT_ATTN_X3")) gpt_attn_x3 = atoi(e) != 0;
     if (const char* e = getenv("DDMI_FUSE_POOL")) fuse_pool = atoi(e) != 0;
     if (const char* e = getenv("DDMI_MK_STAMPS")) mk_stamps = atoi(e) != 0;
@@ -1730,6 +1732,15 @@ class Model {
         t.query_out = q;
         t.B = B;
         t.flags = num_flags;
+        // four workgroups per scene (heads / FFN chunks split, three L2 exchanges per layer) while B x 4 fits a
+        // quarter of the chip: batch 1 2.745 -> 2.62 ms, but at B = 64 the 256 mostly-waiting workgroups crowd out
+        // the main stream's work beside them (3 in flight -1.5 %, profiles/round5_ab.md). DDMI_TF_GROUPS=1 / 4
+        // forces a form; the stamps diagnostics take the one-workgroup kernel
+        t.groups = (mk_stamps || tf_groups_env == 1) ? 1 : ((tf_groups_env == 4 || B * 4 <= 64) ? 4 : 1);
+        if (t.groups == 4) {
+          t.xbuf = buf("tf_xbuf", (size_t)B * 9 * 4 * 32 * d);
+          t.sync_cnt = reinterpret_cast<unsigned*>(buf("tf_sync_cnt", (size_t)B));
+        }
         if (mk_stamps) t.stamps = reinterpret_cast<unsigned long long*>(buf("tf_stamps", (size_t)B * 80));
         // 2 x rows x sum(K x N): per layer q|k|v, 2 out_proj, cross q, FFN (+ the attention products), hoists
         const double kn = 3.0 * (3584.0 * d) + 4.0 * d * d + 4.0 * d * d;

@@ -361,6 +361,288 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk_kernel(TfMkArgs a) {
 #endif
 }
 
+// ================================================================================================
+// Four workgroups per scene (TfMkArgs::groups = 4). One workgroup streams every weight of the layer stack
+// through its 8 waves' rings at the latency of its in-flight loads (~12.5 MB at ~45 GB/s: 0.3 ms, batch 1);
+// here workgroup g of a scene takes
+//   * heads 2g, 2g+1 of both attentions (their q | k | v / q column tiles: 6 and 2 waves),
+//   * hidden chunk g (columns 256 g ..) of FFN linear1 and that K-slice of linear2 as a partial sum,
+//   * one quarter of the trajectory-head hoists (g 0, 1: agent K | V of diffusion layer g; g 2, 3: the ego
+//     chain of layer g - 2),
+// and every workgroup runs the out_projs, residuals and LayerNorms on the full rows itself (identical inputs,
+// identical arithmetic: identical results), so a layer exchanges three times through L2: the two attention
+// outputs (each workgroup's 64 columns) and the four linear2 partials, summed in slab order 0..3 by every
+// workgroup. Per wave a layer is 6 weight-streaming GEMM units instead of 14. The linear2 sum order differs
+// from the one-workgroup kernel's single accumulation chain (fp32 rounding level; checked against the unfused
+// chain and the goldens like it).
+constexpr int tG = 4;
+constexpr int XSLAB = 32 * tD;   // one [32][256] fp32 slab
+constexpr int XBUF = tG * XSLAB;  // one exchange buffer (the linear2 partials take all four slabs)
+constexpr int tNX = 3 * tL;       // exchanges per launch, each with a buffer of its own: a workgroup never reads
+                                  // a line it (or its XCD's L2) read earlier in the launch, whose stale copy the
+                                  // per-XCD L2 could serve after another XCD rewrote it
+
+// Barrier of the scene's tG workgroups (MI355X_MICROARCH.md, inter-workgroup visibility): every wave's stores
+// drained, workgroup barrier, lane 0: agent release + vmcnt(0), relaxed arrival add, relaxed poll until the
+// counter reaches target (monotonic within a launch: the n-th barrier waits for n * tG arrivals), agent
+// acquire + vmcnt(0); workgroup barrier. A wait that outlives any healthy schedule raises a flag and goes on
+// rather than hang the device.
+__device__ inline void scene_sync(unsigned* cnt, unsigned target, unsigned* flags) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned n = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++n == (1u << 22)) {
+        if (flags) atomicOr(flags, DD_NUM_SYNC_TIMEOUT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// head h's output O[query][h * 32 + dim] from o (C layout) into an fp32 exchange slab; rows >= 31 zero
+__device__ inline void put_head_out(float* slab, int h, const mk_f16& o) {
+  const int lane = threadIdx.x & 63, q = lane & 31, hh = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int dim = (r & 3) + 8 * (r >> 2) + 4 * hh;
+    slab[q * tD + h * tHD + dim] = q < tQ ? o[r] : 0.f;
+  }
+}
+
+// a [32][256] fp32 slab into a split image
+__device__ inline void get_rows_split(const float* slab, char* dst) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = threadIdx.x + NT * k;
+    const int row = e >> 6, c4 = (e & 63) * 4;
+    st_split4(dst, HP, row, c4, *reinterpret_cast<const float4*>(slab + row * tD + c4));
+  }
+}
+
+__global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* XS = lds;
+  float* R1 = reinterpret_cast<float*>(lds + REG);
+  char* R2 = lds + 2 * REG;
+  char* R3 = lds + 3 * REG;
+  const int b = blockIdx.x / tG, g = blockIdx.x - (blockIdx.x / tG) * tG;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, hh = lane >> 5;
+  const MkLin none{};
+  const float scale = 1.0f / sqrtf((float)tHD);
+  unsigned* cnt = a.sync_cnt + b;
+  float* xb = a.xbuf + (int64_t)b * tNX * XBUF;
+  unsigned nsync = 0;
+  auto sync = [&]() {
+    ++nsync;
+    scene_sync(cnt, nsync * tG, a.flags);
+  };
+  auto xbuf_next = [&]() { return xb + nsync * XBUF; };  // exchange n writes buffer n
+  const __attribute__((address_space(4))) TfMkLayer* lay = (const __attribute__((address_space(4))) TfMkLayer*)a.layers;
+  // this wave's tiles: self-attention q | k | v unit wave / 2 of head 2g + (wave & 1) (waves 0..5), cross q of
+  // head 2g + wave (waves 0, 1), FFN hidden tile wave of chunk g
+  const int qkv_nt = (wave >> 1) * 8 + 2 * g + (wave & 1);
+  const int caq_nt = 2 * g + wave;
+  const int l1_nt = 8 * g + wave;
+  Ring R;
+  if (wave < 6) ring_fill(R, ld_lin(lay[0].sa_in), qkv_nt, 0);
+
+  for (int e = tid; e < 32 * 64; e += NT) {
+    const int q = e >> 6, c4 = (e & 63) * 4;
+    const float4 v = q < tQ ? *reinterpret_cast<const float4*>(a.qemb + q * tD + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    st_split4(XS, HP, q, c4, v);
+  }
+  __syncthreads();
+
+  mk_f16 acc, acc2;
+#pragma unroll 1
+  for (int l = 0; l < tL; ++l) {
+    TfMkLayer L;
+    {
+      const __attribute__((address_space(4))) TfMkLayer& c = lay[l];
+      L.sa_in = ld_lin(c.sa_in);
+      L.sa_out = ld_lin(c.sa_out);
+      L.ca_q = ld_lin(c.ca_q);
+      L.ca_out = ld_lin(c.ca_out);
+      L.l1 = ld_lin(c.l1);
+      L.l2 = ld_lin(c.l2);
+      L.n1g = c.n1g;
+      L.n1b = c.n1b;
+      L.n2g = c.n2g;
+      L.n2b = c.n2b;
+      L.n3g = c.n3g;
+      L.n3b = c.n3b;
+    }
+    // ============================================================ self-attention, heads 2g, 2g+1
+    float* Qf = R1;
+    float* Kf = reinterpret_cast<float*>(R2);
+    float* Vf = reinterpret_cast<float*>(R3);
+    if (wave < 6) {
+      const int u = wave >> 1;
+      zero_acc(acc);
+      mk_gemm<16>(XS, XS + SPB, HP, L.sa_in, qkv_nt, 0, acc, 0, R, none, 0, 0);
+      float* dst = u == 0 ? Qf : (u == 1 ? Kf : Vf);
+      mk_epi<tQ>(acc, L.sa_in, qkv_nt, a.flags, [&](int row, int col, float v) { dst[row * FP + col - u * tD] = v; });
+    }
+    __syncthreads();
+    float* xo = xbuf_next();
+    if (wave < 2) {
+      const int h = 2 * g + wave;
+      float qf[2][8];
+      load_q_frags(Qf, h, qf);
+      mk_f16 sc;
+      zero_acc(sc);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float a8[8];
+        ld8(Kf + li * FP + h * tHD + 16 * ks + 8 * hh, a8);
+        mfma6(sc, a8, qf[ks]);
+      }
+      mk_f16 st[3];
+      st[0] = sc;
+      softmax_keys<1>(st, tQ, scale);
+      mk_f16 o;
+      zero_acc(o);
+      attn_pv_t<1>(st, o, [&](int key) { return Vf + key * FP + h * tHD; }, tQ);
+      put_head_out(xo, h, o);
+    }
+    ring_fill(R, L.sa_out, wave, 0);
+    sync();
+    get_rows_split(xo, R2);
+    __syncthreads();
+    // out_proj + residual -> R1; norm1 -> XS (every workgroup, full rows)
+    zero_acc(acc);
+    mk_gemm<16>(R2, R2 + SPB, HP, L.sa_out, wave, 0, acc, 0, R, wave < 2 ? L.ca_q : none, wave < 2 ? caq_nt : 0, 0);
+    mk_epi<tQ>(acc, L.sa_out, wave, a.flags,
+               [&](int row, int col, float v) { R1[row * FP + col] = v + xres(XS, row, col); });
+    __syncthreads();
+    ln_rows(R1, L.n1g, L.n1b, XS, nullptr);
+    __syncthreads();
+
+    // ============================================================ cross-attention, heads 2g, 2g+1
+    float* Qc = reinterpret_cast<float*>(R2);
+    if (wave < 2) {
+      zero_acc(acc);
+      mk_gemm<16>(XS, XS + SPB, HP, L.ca_q, caq_nt, 0, acc, 0, R, none, 0, 0);
+      mk_epi<tQ>(acc, L.ca_q, caq_nt, a.flags, [&](int row, int col, float v) { Qc[row * FP + col] = v; });
+    }
+    __syncthreads();
+    xo = xbuf_next();
+    if (wave < 2) {
+      const int h = 2 * g + wave;
+      const float* kvx = a.kvx + (int64_t)b * tM * 1536 + l * 512;
+      float qf[2][8];
+      load_q_frags(Qc, h, qf);
+      mk_f16 st[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        zero_acc(st[t]);
+        const int key = 32 * t + li;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          float a8[8];
+          if (key < tM) {
+            ld8(kvx + (int64_t)key * 1536 + h * tHD + 16 * ks + 8 * hh, a8);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] = 0.f;
+          }
+          mfma6(st[t], a8, qf[ks]);
+        }
+      }
+      softmax_keys<3>(st, tM, scale);
+      mk_f16 o;
+      zero_acc(o);
+      attn_pv_t<3>(st, o, [&](int key) { return kvx + (int64_t)key * 1536 + tD + h * tHD; }, tM);
+      put_head_out(xo, h, o);
+    }
+    ring_fill(R, L.ca_out, wave, 0);
+    sync();
+    get_rows_split(xo, R2);
+    __syncthreads();
+    zero_acc(acc);
+    mk_gemm<16>(R2, R2 + SPB, HP, L.ca_out, wave, 0, acc, 0, R, L.l1, l1_nt, 0);
+    mk_epi<tQ>(acc, L.ca_out, wave, a.flags,
+               [&](int row, int col, float v) { R1[row * FP + col] = v + xres(XS, row, col); });
+    __syncthreads();
+    ln_rows(R1, L.n2g, L.n2b, XS, nullptr);
+    __syncthreads();
+
+    // ============================================================ FFN: hidden chunk g, its linear2 partial
+    zero_acc(acc);
+    mk_gemm<16>(XS, XS + SPB, HP, L.l1, l1_nt, 0, acc, 0, R, L.l2, wave, g * 16);
+    mk_epi<tQ>(acc, L.l1, l1_nt, a.flags,
+               [&](int row, int col, float v) { st_split(R2, HP, row, col - g * tD, row < tQ ? fmaxf(v, 0.f) : 0.f); });
+    __syncthreads();
+    zero_acc(acc2);
+    {
+      MkLin nx = none;
+      int nnt = 0;
+      if (l + 1 < tL) {
+        if (wave < 6) {
+          nx = ld_lin(lay[l + 1].sa_in);
+          nnt = qkv_nt;
+        }
+      } else {
+        nx = g < 2 ? a.ag_kv[g] : a.eg_v[g - 2];
+        nnt = wave;
+      }
+      mk_gemm<16>(R2, R2 + SPB, HP, L.l2, wave, g * 16, acc2, 0, R, nx, nnt, 0);
+    }
+    float* xp = xbuf_next();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xp[g * XSLAB + ((r & 3) + 8 * (r >> 2) + 4 * hh) * tD + wave * 32 + li] = acc2[r];
+    sync();
+    // every workgroup: x = LN3(x + (p0 + p1 + p2 + p3) s + b), its waves summing their own tiles' partials
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = ((r & 3) + 8 * (r >> 2) + 4 * hh) * tD + wave * 32 + li;
+      acc2[r] = ((xp[o] + xp[XSLAB + o]) + xp[2 * XSLAB + o]) + xp[3 * XSLAB + o];
+    }
+    mk_epi<tQ>(acc2, L.l2, wave, a.flags,
+               [&](int row, int col, float v) { R1[row * FP + col] = v + xres(XS, row, col); });
+    __syncthreads();
+    ln_rows(R1, L.n3g, L.n3b, XS, (l + 1 == tL && g == 0) ? a.query_out + (int64_t)b * tQ * tD : nullptr);
+    __syncthreads();
+  }
+
+  // ============================================================ hoists of the trajectory head, a quarter each
+  if (g < 2) {
+    // agent K | V of diffusion layer d = g (rows 1..30 = the agent queries)
+    const int d = g;
+    float* out = a.akv[d] + (int64_t)b * 30 * 512;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int nt = u * 8 + wave;
+      zero_acc(acc);
+      mk_gemm<16>(XS, XS + SPB, HP, a.ag_kv[d], nt, 0, acc, 0, R, u == 0 ? a.ag_kv[d] : none, u == 0 ? nt + 8 : 0, 0);
+      mk_epi<tQ>(acc, a.ag_kv[d], nt, a.flags, [&](int row, int col, float v) {
+        if (row >= 1 && row < tQ) out[(row - 1) * 512 + col] = v;
+      });
+    }
+  } else {
+    // ego of diffusion layer d = g - 2: out_proj(v_proj(query row 0))
+    const int d = g - 2;
+    zero_acc(acc);
+    mk_gemm<16>(XS, XS + SPB, HP, a.eg_v[d], wave, 0, acc, 0, R, a.eg_out[d], wave, 0);
+    mk_epi<1>(acc, a.eg_v[d], wave, a.flags, [&](int row, int col, float v) { st_split(R2, HP, row, col, row == 0 ? v : 0.f); });
+    __syncthreads();
+    zero_acc(acc);
+    mk_gemm<16>(R2, R2 + SPB, HP, a.eg_out[d], wave, 0, acc, 0, R, none, 0, 0);
+    mk_epi<1>(acc, a.eg_out[d], wave, a.flags, [&](int row, int col, float v) {
+      if (row == 0) a.ego[d][(int64_t)b * tD + col] = v;
+    });
+  }
+}
+
 }  // namespace
 
 bool tfdec_mk_layer_ok(const TfMkLayer& L) {
@@ -376,6 +658,17 @@ void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st) {
   if (a.B <= 0) return;
   if (!a.layers || !a.qemb || !a.kvx || !a.query_out || !a.akv[0] || !a.akv[1] || !a.ego[0] || !a.ego[1])
     throw std::runtime_error("tfdec_mk: missing operand");
+  if (a.groups == tG) {
+    if (!a.xbuf || !a.sync_cnt) throw std::runtime_error("tfdec_mk: groups = 4 needs xbuf / sync_cnt");
+    static std::atomic<uint64_t> attr4;
+    set_max_lds_once(attr4, reinterpret_cast<const void*>(tfdec_mk4_kernel), LDS_T);
+    // the scene counters start every launch at zero (a memset node in the captured graph)
+    DD_HIP_CHECK(hipMemsetAsync(a.sync_cnt, 0, (size_t)a.B * sizeof(unsigned), st));
+    hipLaunchKernelGGL(tfdec_mk4_kernel, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
+    DD_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (a.groups != 1) throw std::runtime_error("tfdec_mk: groups must be 1 or 4");
   static std::atomic<uint64_t> attr;
   set_max_lds_once(attr, reinterpret_cast<const void*>(tfdec_mk_kernel), LDS_T);
   hipLaunchKernelGGL(tfdec_mk_kernel, dim3(a.B), dim3(NT), LDS_T, st, a);

@@ -184,8 +184,11 @@ int dd_get_gemm_mode(dd_handle* h, int* mode);
 int dd_set_schedule(dd_handle* h, int schedule);
 /* Numerics flags raised by kernels since the last clear (synchronises the handle's stream):
  * bit 0 (DD_NUM_F16_OVERFLOW_BIT) = an activation reached |x| >= 65504 under DD_GEMM_F16X3, so that
- * forward's result is not trustworthy (re-run it in DD_GEMM_FP32). clear != 0 resets them. */
+ * forward's result is not trustworthy (re-run it in DD_GEMM_FP32); bit 1 (DD_NUM_SYNC_TIMEOUT_BIT) = the
+ * tf-decoder megakernel's inter-workgroup wait gave up (never on a healthy device; same remedy).
+ * clear != 0 resets them. */
 #define DD_NUM_F16_OVERFLOW_BIT 1u
+#define DD_NUM_SYNC_TIMEOUT_BIT 2u
 int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear);
 /* Copy a named internal buffer (e.g. "p3", "keyval", "cross_bev", "reg_s0l1") of the last
  * forward into dst (device pointer), at most `count` floats; *actual = buffer length. */
