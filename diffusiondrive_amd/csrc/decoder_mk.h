@@ -121,7 +121,7 @@ struct TfMkArgs {
   float* ego[2] = {nullptr, nullptr};  // [B][256]
   int B = 0;
   // groups = 4: four workgroups per scene (heads / hidden chunks split over them, exchanges through xbuf):
-  // xbuf [B][9][4][32][256] floats (one buffer per exchange), sync_cnt [B] zeroed by the launcher
+  // xbuf [B][9][4][32][256] floats (one buffer per exchange), sync_cnt [2B] (arrivals, finishes) zeroed at allocation
   int groups = 1;
   float* xbuf = nullptr;
   unsigned* sync_cnt = nullptr;

@@ -1739,7 +1739,7 @@ class Model {
         t.groups = (mk_stamps || tf_groups_env == 1) ? 1 : ((tf_groups_env == 4 || B * 4 <= 64) ? 4 : 1);
         if (t.groups == 4) {
           t.xbuf = buf("tf_xbuf", (size_t)B * 9 * 4 * 32 * d);
-          t.sync_cnt = reinterpret_cast<unsigned*>(buf("tf_sync_cnt", (size_t)B));
+          t.sync_cnt = reinterpret_cast<unsigned*>(buf_zeroed("tf_sync_cnt", (size_t)2 * B));
         }
         if (mk_stamps) t.stamps = reinterpret_cast<unsigned long long*>(buf("tf_stamps", (size_t)B * 80));
         // 2 x rows x sum(K x N): per layer q|k|v, 2 out_proj, cross q, FFN (+ the attention products), hoists

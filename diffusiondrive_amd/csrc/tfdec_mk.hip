@@ -387,11 +387,13 @@ constexpr int tNX = 3 * tL;       // exchanges per launch, each with a buffer of
 // counter reaches target (monotonic within a launch: the n-th barrier waits for n * tG arrivals), agent
 // acquire + vmcnt(0); workgroup barrier. A wait that outlives any healthy schedule raises a flag and goes on
 // rather than hang the device.
+template <bool SYS>
 __device__ inline void scene_sync(unsigned* cnt, unsigned target, unsigned* flags) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if constexpr (SYS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned n = 0;
@@ -402,32 +404,49 @@ __device__ inline void scene_sync(unsigned* cnt, unsigned target, unsigned* flag
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if constexpr (SYS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 }
 
-// head h's output O[query][h * 32 + dim] from o (C layout) into an fp32 exchange slab; rows >= 31 zero
-__device__ inline void put_head_out(float* slab, int h, const mk_f16& o) {
+// Exchange data moves with sc1 (write-through) stores and sc1 loads through a buffer resource over the scene's
+// exchange area, as value_proj's split partials (MI355X_MICROARCH.md hand-off table)
+constexpr int kXSC1 = 16;
+__device__ inline __amdgpu_buffer_rsrc_t xrsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// head h's output O[query][h * 32 + dim] from o (C layout) into an fp32 exchange slab (float offset so); rows >= 31 zero
+__device__ inline void put_head_out(__amdgpu_buffer_rsrc_t rx, int so, int h, const mk_f16& o) {
   const int lane = threadIdx.x & 63, q = lane & 31, hh = lane >> 5;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int dim = (r & 3) + 8 * (r >> 2) + 4 * hh;
-    slab[q * tD + h * tHD + dim] = q < tQ ? o[r] : 0.f;
+    const float v = q < tQ ? o[r] : 0.f;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rx, (so + q * tD + h * tHD + dim) * 4, 0,
+                                          kXSC1);
   }
 }
 
-// a [32][256] fp32 slab into a split image
-__device__ inline void get_rows_split(const float* slab, char* dst) {
+// a [32][256] fp32 exchange slab (float offset so) into a split image
+__device__ inline void get_rows_split(__amdgpu_buffer_rsrc_t rx, int so, char* dst) {
+  float4 v[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int e = threadIdx.x + NT * k;
     const int row = e >> 6, c4 = (e & 63) * 4;
-    st_split4(dst, HP, row, c4, *reinterpret_cast<const float4*>(slab + row * tD + c4));
+    v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, (so + row * tD + c4) * 4, 0, kXSC1));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = threadIdx.x + NT * k;
+    st_split4(dst, HP, e >> 6, (e & 63) * 4, v[k]);
   }
 }
 
+template <bool SYS>
 __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* XS = lds;
@@ -439,13 +458,13 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   const MkLin none{};
   const float scale = 1.0f / sqrtf((float)tHD);
   unsigned* cnt = a.sync_cnt + b;
-  float* xb = a.xbuf + (int64_t)b * tNX * XBUF;
+  const __amdgpu_buffer_rsrc_t rx = xrsrc(a.xbuf + (int64_t)b * tNX * XBUF);
   unsigned nsync = 0;
   auto sync = [&]() {
     ++nsync;
-    scene_sync(cnt, nsync * tG, a.flags);
+    scene_sync<SYS>(cnt, nsync * tG, a.flags);
   };
-  auto xbuf_next = [&]() { return xb + nsync * XBUF; };  // exchange n writes buffer n
+  auto xbuf_next = [&]() { return (int)nsync * XBUF; };  // exchange n writes buffer n (float offset)
   const __attribute__((address_space(4))) TfMkLayer* lay = (const __attribute__((address_space(4))) TfMkLayer*)a.layers;
   // this wave's tiles: self-attention q | k | v unit wave / 2 of head 2g + (wave & 1) (waves 0..5), cross q of
   // head 2g + wave (waves 0, 1), FFN hidden tile wave of chunk g
@@ -493,7 +512,7 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
       mk_epi<tQ>(acc, L.sa_in, qkv_nt, a.flags, [&](int row, int col, float v) { dst[row * FP + col - u * tD] = v; });
     }
     __syncthreads();
-    float* xo = xbuf_next();
+    int xo = xbuf_next();
     if (wave < 2) {
       const int h = 2 * g + wave;
       float qf[2][8];
@@ -512,11 +531,11 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
       mk_f16 o;
       zero_acc(o);
       attn_pv_t<1>(st, o, [&](int key) { return Vf + key * FP + h * tHD; }, tQ);
-      put_head_out(xo, h, o);
+      put_head_out(rx, xo, h, o);
     }
     ring_fill(R, L.sa_out, wave, 0);
     sync();
-    get_rows_split(xo, R2);
+    get_rows_split(rx, xo, R2);
     __syncthreads();
     // out_proj + residual -> R1; norm1 -> XS (every workgroup, full rows)
     zero_acc(acc);
@@ -562,11 +581,11 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
       mk_f16 o;
       zero_acc(o);
       attn_pv_t<3>(st, o, [&](int key) { return kvx + (int64_t)key * 1536 + tD + h * tHD; }, tM);
-      put_head_out(xo, h, o);
+      put_head_out(rx, xo, h, o);
     }
     ring_fill(R, L.ca_out, wave, 0);
     sync();
-    get_rows_split(xo, R2);
+    get_rows_split(rx, xo, R2);
     __syncthreads();
     zero_acc(acc);
     mk_gemm<16>(R2, R2 + SPB, HP, L.ca_out, wave, 0, acc, 0, R, L.l1, l1_nt, 0);
@@ -597,15 +616,23 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
       }
       mk_gemm<16>(R2, R2 + SPB, HP, L.l2, wave, g * 16, acc2, 0, R, nx, nnt, 0);
     }
-    float* xp = xbuf_next();
+    const int xp = xbuf_next();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) xp[g * XSLAB + ((r & 3) + 8 * (r >> 2) + 4 * hh) * tD + wave * 32 + li] = acc2[r];
+    for (int r = 0; r < 16; ++r) {
+      const unsigned u = __builtin_bit_cast(unsigned, (float)acc2[r]);
+      __builtin_amdgcn_raw_buffer_store_b32(u, rx, (xp + g * XSLAB + ((r & 3) + 8 * (r >> 2) + 4 * hh) * tD + wave * 32 + li) * 4,
+                                            0, kXSC1);
+    }
     sync();
     // every workgroup: x = LN3(x + (p0 + p1 + p2 + p3) s + b), its waves summing their own tiles' partials
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int o = ((r & 3) + 8 * (r >> 2) + 4 * hh) * tD + wave * 32 + li;
-      acc2[r] = ((xp[o] + xp[XSLAB + o]) + xp[2 * XSLAB + o]) + xp[3 * XSLAB + o];
+      const int o = (xp + ((r & 3) + 8 * (r >> 2) + 4 * hh) * tD + wave * 32 + li) * 4;
+      float p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        p[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, o + j * XSLAB * 4, 0, kXSC1));
+      acc2[r] = ((p[0] + p[1]) + p[2]) + p[3];
     }
     mk_epi<tQ>(acc2, L.l2, wave, a.flags,
                [&](int row, int col, float v) { R1[row * FP + col] = v + xres(XS, row, col); });
@@ -614,6 +641,14 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
     __syncthreads();
   }
 
+  // every workgroup of the scene is past its last wait: the last to get here resets the scene's counters
+  if (tid == 0) {
+    unsigned* done = a.sync_cnt + a.B + b;
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tG - 1) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   // ============================================================ hoists of the trajectory head, a quarter each
   if (g < 2) {
     // agent K | V of diffusion layer d = g (rows 1..30 = the agent queries)
@@ -660,11 +695,19 @@ void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st) {
     throw std::runtime_error("tfdec_mk: missing operand");
   if (a.groups == tG) {
     if (!a.xbuf || !a.sync_cnt) throw std::runtime_error("tfdec_mk: groups = 4 needs xbuf / sync_cnt");
-    static std::atomic<uint64_t> attr4;
-    set_max_lds_once(attr4, reinterpret_cast<const void*>(tfdec_mk4_kernel), LDS_T);
-    // the scene counters start every launch at zero (a memset node in the captured graph)
-    DD_HIP_CHECK(hipMemsetAsync(a.sync_cnt, 0, (size_t)a.B * sizeof(unsigned), st));
-    hipLaunchKernelGGL(tfdec_mk4_kernel, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
+    static std::atomic<uint64_t> attr4, attr4s;
+    // the scene counters start at zero (zeroed at allocation) and the last workgroup of a scene to finish resets
+    // them; DDMI_TF_MEMSET=1 also zeroes them ahead of every launch (a memset node in the captured graph)
+    const char* me = getenv("DDMI_TF_MEMSET");
+    if (me && atoi(me)) DD_HIP_CHECK(hipMemsetAsync(a.sync_cnt, 0, (size_t)a.B * 2 * sizeof(unsigned), st));
+    const char* se = getenv("DDMI_TF_SYS");  // diagnostic: system-scope fences at the exchanges
+    if (se && atoi(se)) {
+      set_max_lds_once(attr4s, reinterpret_cast<const void*>(tfdec_mk4_kernel<true>), LDS_T);
+      hipLaunchKernelGGL(tfdec_mk4_kernel<true>, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
+    } else {
+      set_max_lds_once(attr4, reinterpret_cast<const void*>(tfdec_mk4_kernel<false>), LDS_T);
+      hipLaunchKernelGGL(tfdec_mk4_kernel<false>, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
+    }
     DD_HIP_CHECK(hipGetLastError());
     return;
   }
