@@ -382,18 +382,16 @@ constexpr int tNX = 3 * tL;       // exchanges per launch, each with a buffer of
                                   // a line it (or its XCD's L2) read earlier in the launch, whose stale copy the
                                   // per-XCD L2 could serve after another XCD rewrote it
 
-// Barrier of the scene's tG workgroups (MI355X_MICROARCH.md, inter-workgroup visibility): every wave's stores
-// drained, workgroup barrier, lane 0: agent release + vmcnt(0), relaxed arrival add, relaxed poll until the
-// counter reaches target (monotonic within a launch: the n-th barrier waits for n * tG arrivals), agent
-// acquire + vmcnt(0); workgroup barrier. A wait that outlives any healthy schedule raises a flag and goes on
-// rather than hang the device.
-template <bool SYS>
+// Barrier of the scene's tG workgroups (MI355X_MICROARCH.md, inter-workgroup visibility): every wave's (sc1)
+// stores drained, workgroup barrier, lane 0: agent release + vmcnt(0), relaxed arrival add, relaxed poll until
+// the counter reaches target (monotonic within a launch: the n-th barrier waits for n * tG arrivals), agent
+// acquire + vmcnt(0); workgroup barrier; then sc1 loads. A wait that outlives any healthy schedule raises a flag
+// and goes on rather than hang the device.
 __device__ inline void scene_sync(unsigned* cnt, unsigned target, unsigned* flags) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    if constexpr (SYS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned n = 0;
@@ -404,8 +402,7 @@ __device__ inline void scene_sync(unsigned* cnt, unsigned target, unsigned* flag
         break;
       }
     }
-    if constexpr (SYS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -446,7 +443,6 @@ __device__ inline void get_rows_split(__amdgpu_buffer_rsrc_t rx, int so, char* d
   }
 }
 
-template <bool SYS>
 __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* XS = lds;
@@ -462,7 +458,7 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   unsigned nsync = 0;
   auto sync = [&]() {
     ++nsync;
-    scene_sync<SYS>(cnt, nsync * tG, a.flags);
+    scene_sync(cnt, nsync * tG, a.flags);
   };
   auto xbuf_next = [&]() { return (int)nsync * XBUF; };  // exchange n writes buffer n (float offset)
   const __attribute__((address_space(4))) TfMkLayer* lay = (const __attribute__((address_space(4))) TfMkLayer*)a.layers;
@@ -695,19 +691,13 @@ void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st) {
     throw std::runtime_error("tfdec_mk: missing operand");
   if (a.groups == tG) {
     if (!a.xbuf || !a.sync_cnt) throw std::runtime_error("tfdec_mk: groups = 4 needs xbuf / sync_cnt");
-    static std::atomic<uint64_t> attr4, attr4s;
+    static std::atomic<uint64_t> attr4;
     // the scene counters start at zero (zeroed at allocation) and the last workgroup of a scene to finish resets
     // them; DDMI_TF_MEMSET=1 also zeroes them ahead of every launch (a memset node in the captured graph)
     const char* me = getenv("DDMI_TF_MEMSET");
     if (me && atoi(me)) DD_HIP_CHECK(hipMemsetAsync(a.sync_cnt, 0, (size_t)a.B * 2 * sizeof(unsigned), st));
-    const char* se = getenv("DDMI_TF_SYS");  // diagnostic: system-scope fences at the exchanges
-    if (se && atoi(se)) {
-      set_max_lds_once(attr4s, reinterpret_cast<const void*>(tfdec_mk4_kernel<true>), LDS_T);
-      hipLaunchKernelGGL(tfdec_mk4_kernel<true>, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
-    } else {
-      set_max_lds_once(attr4, reinterpret_cast<const void*>(tfdec_mk4_kernel<false>), LDS_T);
-      hipLaunchKernelGGL(tfdec_mk4_kernel<false>, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
-    }
+    set_max_lds_once(attr4, reinterpret_cast<const void*>(tfdec_mk4_kernel), LDS_T);
+    hipLaunchKernelGGL(tfdec_mk4_kernel, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
     DD_HIP_CHECK(hipGetLastError());
     return;
   }
