@@ -75,7 +75,7 @@ KERNEL_DESC = {
 }
 CONV_KERNELS = ("conv_x6", "conv_x5", "conv_x3", "conv_gemm", "basicblock")
 OTHER_KERNELS = ("value_proj", "stem_pool", "attn", "layernorm", "softmax", "bilinear", "pool", "mha", "bev_sample",
-                 "decoder", "tfdec", "bevproj", "misc")
+                 "decoder", "tfdec", "bevproj", "gpt_tail", "misc")
 DTYPE = {
     "fp32": "fp32",
     "f16x3": "fp32 via f16x3 (each fp32 operand = hi+lo fp16, products ah*bh+ah*bl+al*bh, fp32 accumulate)",

@@ -366,6 +366,27 @@ void launch_layernorm(const float* x, int64_t ldx, const float* res, int64_t ldr
 // T <= 512, hs in {16, ..., 512}.
 // prec 0: fp32 MFMA; 1: f16x3 MFMA (three-way split scores), the f16x3 / bf16 modes
 void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, float* y, int prec, hipStream_t st);
+// Fused GPT block tail at C = 64 / 128 (gpt_tail.hip): x += proj(y); h = ln2(x); x += mlp(h); hb = lnn(x) in one
+// launch over M token rows, f16x3 products bit-identical to the unfused conv_x3 / conv_x5 chain.
+struct GptTailW {
+  const uint16_t* wh = nullptr;  // pre-split fp16 hi / lo images [N][ldh] (weights.cpp prep_split)
+  const uint16_t* wl = nullptr;
+  const float* sinv = nullptr;   // per-output-channel inverse weight scale
+  const float* bias = nullptr;
+  int ldh = 0;
+  float alpha = 1.0f;
+};
+struct GptTailArgs {
+  const float* y = nullptr;  // [M][C] attention output
+  float* x = nullptr;        // [M][C] residual stream, updated in place
+  float* hb = nullptr;       // [M][C] lnn(x) out
+  int M = 0, C = 0;
+  GptTailW proj, up, down;   // [C][C], [4C][C], [C][4C]
+  const float *ln2_g = nullptr, *ln2_b = nullptr, *lnn_g = nullptr, *lnn_b = nullptr;
+  unsigned* flags = nullptr;
+};
+bool gpt_tail_supported(int C);
+void launch_gpt_tail(const GptTailArgs& a, hipStream_t st);
 // Row softmax of (scale * x), in place, rows of length L (<= 1024), row stride ld.
 void launch_softmax_rows(float* x, int64_t ld, int rows, int L, float scale, hipStream_t st);
 // dst[r][:] = src[r % nsrc][:] for r < rows (row length C, contiguous).

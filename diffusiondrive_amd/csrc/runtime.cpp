@@ -212,6 +212,7 @@ class Model {
   // channel group (value_proj.hip vproj_union_kernel); 0 = every (row, tap) gathered per K chunk
   bool vproj_union = true;
   bool ln_fold = true;  // DDMI_LN_FOLD=0: every GPT LayerNorm as its own launch (gemm_ln)
+  int gpt_tail_env = -1;  // DDMI_GPT_TAIL=0 / 1: force the C <= 128 GPT block tail off / on (default: B <= 16)
   // DDMI_BB_FUSE=1: layer-1 BasicBlocks as one launch each (fused_block, basicblock.hip). Off by default: measured
   // 2.37 ms per forward against 2.06 for the two conv_x6 launches per block (profiles/round5_c_bench.json: one
   // workgroup per CU runs its phases back to back, 39.5 us per tile against ~16 us of MFMA work)
@@ -347,6 +348,7 @@ class Model {
     if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
     if (const char* e = getenv("DDMI_LN_FOLD")) ln_fold = atoi(e) != 0;
+    if (const char* e = getenv("DDMI_GPT_TAIL")) gpt_tail_env = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BB_FUSE")) bb_fuse = std::max(0, std::min(3, atoi(e)));
     if (const char* e = getenv("DDMI_S0_CHUNK_MB")) s0_chunk_mb = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
@@ -1526,11 +1528,44 @@ class Model {
                             ? 0
                             : (gemm_mode == DD_GEMM_BF16 ? 2 : 1);
       launch("attn", 4.0 * B * T * T * (double)C, [&] { launch_gpt_attention(QKV, B, T, C, 4, Y, aprec, st); });
+      const LNp& nx = bi + 1 < g.blocks.size() ? g.blocks[bi + 1].ln1 : g.lnf;
+      // C <= 128 in f16x3 at small batches: proj + ln2 + MLP + the next LayerNorm as one launch (gpt_tail.hip,
+      // bit-identical): 3 launches -> 1 per block (C1 2.623 -> 2.600 ms); at B = 64 the fused launch's longer
+      // dependent chain measured 0.3 % slower than the three kernels (profiles/round5_ab.md)
+      const bool tail_on = gpt_tail_env >= 0 ? gpt_tail_env != 0 : B <= 16;
+      if (tail_on && ln_fold && gemm_mode == DD_GEMM_F16X3 && gpt_tail_supported(C) && w.ln2.c == C && nx.c == C &&
+          w.proj.x3.hi != kNone && w.mlp0.x3.hi != kNone && w.mlp2.x3.hi != kNone) {
+        auto tw = [&](const Lin& L) {
+          GptTailW t;
+          t.wh = reinterpret_cast<const uint16_t*>(W(L.x3.hi));
+          t.wl = reinterpret_cast<const uint16_t*>(W(L.x3.lo));
+          t.sinv = W(L.x3.sinv);
+          t.bias = W(L.b);
+          t.ldh = L.x3.ldh;
+          return t;
+        };
+        GptTailArgs t;
+        t.y = Y;
+        t.x = X;
+        t.hb = Hb;
+        t.M = M;
+        t.C = C;
+        t.proj = tw(w.proj);
+        t.up = tw(w.mlp0);
+        t.down = tw(w.mlp2);
+        t.ln2_g = W(w.ln2.g);
+        t.ln2_b = W(w.ln2.b);
+        t.lnn_g = W(nx.g);
+        t.lnn_b = W(nx.b);
+        t.flags = num_flags;
+        launch("gpt_tail", 2.0 * M * 9.0 * C * C, [&] { launch_gpt_tail(t, st); });
+        hb_ready = true;
+        continue;
+      }
       if (!gemm_ln(w.proj, Y, C, M, X, C, X, C, w.ln2, Hb))  // x = x + proj(y); Hb = ln2(x)
         ln(w.ln2, X, C, Hb, C, M);
       gemm(w.mlp0, Hb, C, M, MLP, 4 * C, true);
-      const LNp& nxt = bi + 1 < g.blocks.size() ? g.blocks[bi + 1].ln1 : g.lnf;
-      hb_ready = gemm_ln(w.mlp2, MLP, 4 * C, M, X, C, X, C, nxt, Hb);  // x = x + mlp(ln2 x); Hb = next LN(x)
+      hb_ready = gemm_ln(w.mlp2, MLP, 4 * C, M, X, C, X, C, nx, Hb);  // x = x + mlp(ln2 x); Hb = next LN(x)
     }
     if (!hb_ready) ln(g.lnf, X, C, Hb, C, M);  // Hb = ln_f(x): image tokens rows 0..255, lidar 256..319 per scene
     conv(i2l[i], Hb + (size_t)nimg * C, (int64_t)T * C, (int64_t)8 * C, C, B, 8, 8, LO, (int64_t)64 * Cl,

@@ -640,6 +640,42 @@ def test_gpt_layernorm_fold_is_bit_identical(gpu_model, seeded_sd, monkeypatch, 
     assert n_ref - n_fused == 8, (n_ref, n_fused)
 
 
+@pytest.mark.parametrize("B", [3, 64])
+def test_gpt_tail_fusion_is_bit_identical(gpu_model, seeded_sd, monkeypatch, B):
+    """The C <= 128 GPT blocks' tail (proj + residual, ln2, MLP-up / ReLU / MLP-down + residual, the next LayerNorm)
+    runs as one launch per block (gpt_tail.hip: the 4C hidden chunk by chunk in LDS) with the unfused chain's
+    products, K order and epilogue expressions: the forward and the last scale's ln_f tokens are bit-identical to the
+    proj / MLP-up / MLP-down launches (DDMI_GPT_TAIL=0), with 4 tail launches per forward in place of 12. The fused
+    form is the default up to B = 16 and forced here (DDMI_GPT_TAIL=1) at B = 64 too."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    inp = synthetic_inputs(B, 57)
+    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
+    nz = torch.from_numpy(inp["noise"]).cuda()
+
+    def run(m):
+        m.set_profiling(True)
+        m.reset_stats()
+        out = m.forward(feats, noise=nz, modes=True)
+        n_tail = m.kernel_stats("gpt_tail")["launches"]
+        m.set_profiling(False)
+        return {k: v.cpu().numpy() for k, v in out.items()}, n_tail, m.tap("gpt_h").cpu().numpy()
+
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DDMI_GPT_TAIL", flag)
+        m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+        try:
+            res[flag] = run(m)
+        finally:
+            m.close()
+    (fused, n_fused, h_fused), (ref, n_ref, h_ref) = res["1"], res["0"]
+    assert n_fused == 4 and n_ref == 0, (n_fused, n_ref)
+    for k in ref:
+        assert np.array_equal(fused[k], ref[k]), k
+    assert np.array_equal(h_fused[: h_ref.size], h_ref[: h_fused.size])
+
+
 def test_fused_basicblock_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
     """Layer 1 of both trunks (stride-1 64-channel BasicBlocks) runs as one launch per block (basicblock.hip: conv1's
     output for the 18 x 18 pixels conv2 reads kept in LDS): the stage outputs, the GPT tokens pooled from the last

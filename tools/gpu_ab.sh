@@ -14,7 +14,7 @@ for rep in $(seq 1 ${REPS:-2}); do
   for cfg in "$@"; do
     env $cfg timeout -k 10 300 python bench.py --no-cpu-baseline --no-compare --steps 100 > gpurun_out/${T}.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { echo "rc=$rc [$cfg]"; tail -5 gpurun_out/${T}.log; exit $rc; }
-    echo "[if3 $cfg] $(tail -1 gpurun_out/${T}.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); m=d["device_ms_per_step"]; print(d["value"], "x5", m.get("conv_x5"), "x6", m.get("conv_x6"), "frac", d["roofline"]["frac"])')"
+    echo "[if3 $cfg] $(tail -1 gpurun_out/${T}.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); m=d["device_ms_per_step"]; print(d["value"], "x5", m.get("conv_x5"), "x6", m.get("conv_x6"), "x3", m.get("conv_x3"), "tail", m.get("gpt_tail"), "frac", d["roofline"]["frac"])')"
     if [ "${IF1:-1}" != "0" ]; then
       env $cfg timeout -k 10 300 python bench.py --in-flight 1 --no-cpu-baseline --no-compare --steps 200 > gpurun_out/${T}1.log 2>&1
       rc=$?; [ $rc -ne 0 ] && { echo "rc=$rc [$cfg]"; tail -5 gpurun_out/${T}1.log; exit $rc; }

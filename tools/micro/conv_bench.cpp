@@ -57,6 +57,11 @@ static const Shape kShapes[] = {
     {"img.l3.s2", 64, 32, 128, 128, 256, 3, 2, 0},
     {"img.l3.ds", 64, 32, 128, 128, 256, 1, 2, 0},
     {"lid.l4.3x3", 64, 8, 8, 512, 512, 3, 1, 1},
+    {"lid.l2.s2", 64, 64, 64, 64, 128, 3, 2, 0},
+    {"lid.l3.s2", 64, 32, 32, 128, 256, 3, 2, 0},
+    {"lid.l4.s2", 64, 16, 16, 256, 512, 3, 2, 0},
+    {"lid.l3.ds", 64, 32, 32, 128, 256, 1, 2, 0},
+    {"lid.l4.ds", 64, 16, 16, 256, 512, 1, 2, 0},
     // fixed-cost probes: the img.l2 / img.l3 tiles with the K walk halved / doubled
     {"fx.l3.c128", 64, 16, 64, 128, 256, 3, 1, 1},
     {"fx.l3.c512", 64, 16, 64, 512, 256, 3, 1, 1},
