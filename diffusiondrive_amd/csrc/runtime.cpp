@@ -348,7 +348,6 @@ class Model {
     if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
     if (const char* e = getenv("DDMI_LN_FOLD")) ln_fold = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_SEG_FORK")) seg_fork = atoi(e) != 0;
     if (const char* e = getenv("DDMI_GPT_TAIL")) gpt_tail_env = atoi(e) != 0;
     if (const char* e = getenv("DDMI_BB_FUSE")) bb_fuse = std::max(0, std::min(3, atoi(e)));
     if (const char* e = getenv("DDMI_S0_CHUNK_MB")) s0_chunk_mb = std::max(0, atoi(e));
@@ -968,17 +967,10 @@ class Model {
   // Segmented capture (capture_program): every launch goes to st_cap under stream capture; fork / join / side close
   // the open segment (a single-stream graph of the launches since the last boundary, tagged with its logical stream),
   // append the event operations and open the next segment.
-  // seg_fork (DDMI_SEG_FORK=1; off by default): a fork does not close the main segment - it records its event
-  // from inside it (an external event-record node) - and side(f) captures the branch on st_side as a graph of its
-  // own; the branch's wait, graph and the main segment's exec op are ordered when the main segment closes at the
-  // join (main exec, then the side's wait / graph / record, then the main's wait): one segment boundary per
-  // branch on the main stream instead of two (each costs the main stream ~15 us of graph-to-graph gap).
   bool seg_cap = false;
-  bool seg_fork = false;  // DDMI_SEG_FORK=1 (experimental: the capture rejects the record, see round5_ab.md)
   int seg_s = 0;
   hipStream_t st_cap = nullptr;
   Program* seg_prog = nullptr;
-  std::vector<SegOp> seg_deferred;  // side ops to run after the open main segment's exec
   void seg_begin(int s) {
     seg_s = s;
     DD_HIP_CHECK(hipStreamBeginCapture(st_cap, hipStreamCaptureModeThreadLocal));
@@ -1009,18 +1001,6 @@ class Model {
   }
   void fork() {
     if (!sides()) return;
-    size_t nd = 0;  // an event-record node needs a node before it in the open main capture
-    if (seg_cap && seg_fork) {
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      DD_HIP_CHECK(hipStreamGetCaptureInfo_v2(st_cap, &cs, nullptr, nullptr, nullptr, &nd));
-    }
-    if (seg_cap && seg_fork && nd > 0) {
-      const int e = (int)fj_next;
-      (void)fj_event();
-      DD_HIP_CHECK(hipEventRecordWithFlags(fj_ev[e], st_cap, hipEventRecordExternal));
-      seg_deferred.push_back({2, 1, nullptr, e});
-      return;
-    }
     if (seg_cap) {
       seg_end();
       seg_event(0, 1);
@@ -1031,15 +1011,10 @@ class Model {
     DD_HIP_CHECK(hipEventRecord(e, st_main));
     DD_HIP_CHECK(hipStreamWaitEvent(st_side, e, 0));
   }
-  void seg_flush() {  // the deferred side ops, after the main segment that records their fork events
-    for (const SegOp& op : seg_deferred) seg_prog->ops.push_back(op);
-    seg_deferred.clear();
-  }
   void join() {
     if (!sides()) return;
     if (seg_cap) {
       seg_end();
-      seg_flush();
       seg_event(1, 0);
       seg_begin(0);
       return;
@@ -1050,34 +1025,6 @@ class Model {
   }
   template <class F>
   void side(F&& f) {
-    if (seg_cap && seg_fork) {  // the branch as a graph of its own, captured on st_side beside the open main capture
-      DD_HIP_CHECK(hipStreamBeginCapture(st_side, hipStreamCaptureModeThreadLocal));
-      st = st_side;
-      try {
-        f();
-      } catch (...) {
-        st = st_cap;
-        hipGraph_t dummy = nullptr;
-        if (hipStreamEndCapture(st_side, &dummy) == hipSuccess && dummy) (void)hipGraphDestroy(dummy);
-        throw;
-      }
-      st = st_cap;
-      hipGraph_t g = nullptr;
-      DD_HIP_CHECK(hipStreamEndCapture(st_side, &g));
-      size_t n = 0;
-      hipError_t e = hipGraphGetNodes(g, nullptr, &n);
-      if (e == hipSuccess && n > 0) {
-        hipGraphExec_t ex = nullptr;
-        e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-        if (e == hipSuccess) {
-          seg_deferred.push_back({0, 1, ex, -1});
-          ++seg_prog->segments;
-        }
-      }
-      (void)hipGraphDestroy(g);
-      DD_HIP_CHECK(e);
-      return;
-    }
     if (seg_cap) {  // launches stay on st_cap; the segment is tagged with the side stream
       seg_end();
       seg_begin(1);
@@ -1101,17 +1048,11 @@ class Model {
     seg_prog = &p;
     st_cap = st;
     seg_cap = sides();
-    seg_deferred.clear();
     try {
       seg_begin(0);
       forward_body(B, steps, heads);
       seg_end();
-      seg_flush();
     } catch (...) {
-      for (const SegOp& op : seg_deferred)
-        if (op.kind == 0 && op.ex) (void)hipGraphExecDestroy(op.ex);
-      seg_deferred.clear();
-      st = st_cap;
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       if (hipStreamIsCapturing(st_cap, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
         hipGraph_t dummy = nullptr;
