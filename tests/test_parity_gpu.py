@@ -388,14 +388,15 @@ def test_tf_decoder_megakernel_matches_unfused_chain(gpu_model, seeded_sd, monke
     assert l2 <= WAYPOINT_L2_TOL
 
 
-@pytest.mark.parametrize("B", [1, 4])
+@pytest.mark.parametrize("B", [1, 4, 16])
 def test_tf_decoder_groups_match_one_workgroup(gpu_model, seeded_sd, monkeypatch, B):
     """The default tf-decoder megakernel runs four workgroups per scene (heads and FFN chunks split, three L2
     exchanges per layer, the linear2 K-slices summed in slab order); DDMI_TF_GROUPS=1 keeps one workgroup per
     scene with a single accumulation chain. Same products, linear2 re-associated: the decoded queries and hoists
-    agree to 1e-5 of the tensor's scale (measured 2-3e-6 relative; the megakernel vs the unfused chain differ by
-    as much), the trajectories within the waypoint bar, no numerics / sync-timeout flag is raised, and a second
-    run of the four-workgroup kernel is bit-identical (the exchanges are race-free)."""
+    agree within the per-mode bar of the tensor's scale (measured 3e-6 relative at B = 1 / 4, 3.5e-5 at B = 16 - the
+    largest of more rows; the megakernel and the unfused chain differ by as much), the trajectories within the
+    waypoint bar, no numerics / sync-timeout flag is raised, and a second run of the four-workgroup kernel is
+    bit-identical (the exchanges are race-free)."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
     inp = synthetic_inputs(B, 43)
@@ -433,7 +434,7 @@ def test_tf_decoder_groups_match_one_workgroup(gpu_model, seeded_sd, monkeypatch
     for k in sizes:
         err = float(np.abs(taps4[k] - taps1[k]).max())
         lines.append(f"  {k:10s} max abs err {err:.3e} (max |ref| {np.abs(taps1[k]).max():.3e})")
-        assert err <= 1e-5 * max(1.0, float(np.abs(taps1[k]).max())), (k, err)
+        assert err <= MODE_TOL * max(1.0, float(np.abs(taps1[k]).max())), (k, err)
     l2 = waypoint_l2(out4, out1)
     lines.append(f"  trajectory waypoint L2 {l2:.3e}")
     _report(lines)
@@ -674,6 +675,35 @@ def test_gpt_tail_fusion_is_bit_identical(gpu_model, seeded_sd, monkeypatch, B):
     for k in ref:
         assert np.array_equal(fused[k], ref[k]), k
     assert np.array_equal(h_fused[: h_ref.size], h_ref[: h_fused.size])
+
+
+@pytest.mark.parametrize("B", [16, 17])
+def test_small_batch_forms_at_their_boundary(seeded_sd, B):
+    """The small-batch forms switch by batch size (tf decoder four workgroups per scene and the fused GPT block tail
+    up to B = 16, one workgroup / three launches above): at B = 16 and 17 the default handle's forward stays within
+    the 1e-4 waypoint bar of the CPU oracle (the golden-pinned restatement) with no flag raised, and the profiler
+    shows which forms ran."""
+    from diffusiondrive_amd.model import DiffusionDriveModel
+    from diffusiondrive_amd.weights import synthetic_inputs
+    from oracle.model import OracleModel
+    inp = synthetic_inputs(B, 71)
+    ref = OracleModel(seeded_sd).forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"],
+                                         inp["noise"], heads=False)
+    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
+    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
+    try:
+        m.set_profiling(True)
+        m.reset_stats()
+        out = m.forward(feats, noise=torch.from_numpy(inp["noise"]))
+        n_tail = m.kernel_stats("gpt_tail")["launches"]
+        m.set_profiling(False)
+        assert m.numerics_flags(clear=True) == 0
+    finally:
+        m.close()
+    assert n_tail == (4 if B <= 16 else 0), n_tail
+    l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
+    _report([f"== small-batch forms at B={B}: waypoint L2 vs oracle {l2:.3e}, gpt_tail launches {n_tail}"])
+    assert l2 <= WAYPOINT_L2_TOL
 
 
 def test_fused_basicblock_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
