@@ -62,6 +62,10 @@ struct ConvArgs {
   int KH = 1, KW = 1, stride = 1, pad = 0;
   int relu = 0;
   float alpha = 1.0f;  // scale applied to the accumulator before bias/res
+  // K-split scratch for conv_x3 at small grids (runtime-owned, one per stream of the forward): S x M x Cout fp32
+  // partials, summed in split order by a reduce launch that applies the epilogue; null: no split
+  float* split_part = nullptr;
+  int64_t split_cap = 0;  // floats
   int batch = 1, zdiv = 1;
   int64_t in_z1 = 0, in_z2 = 0, w_z1 = 0, w_z2 = 0, out_z1 = 0, out_z2 = 0, res_z1 = 0, res_z2 = 0;
   int64_t flops_K = -1;  // algorithmic K per output (excluding channel padding); -1 = KH*KW*Cin

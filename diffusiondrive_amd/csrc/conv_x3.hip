@@ -57,7 +57,9 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0, int GATHER = 0>
+// SPLIT: blockIdx.y = split sp of gridDim.y takes K chunks [nk sp / S, nk (sp + 1) / S) and stores its raw
+// accumulators into ConvArgs::split_part[sp][M][Cout] (x3_split_reduce applies the epilogue)
+template <int WM, int WN, int TM, int TN, int MODE, int PREC = 0, int GATHER = 0, int SPLIT = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % 32 == 0 and KH*KW <= 32 - a 32-wide K chunk lies inside one filter tap, the
@@ -130,6 +132,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   const int in_sh = (int)a.in_sh, in_sw = (int)a.in_sw;
   const int ldh = (int)a.ldh;
   const int Kp = (K + 7) & ~7;
+  // this workgroup's K range (chunks of BK): the whole K, or split sp's slice
+  const int nk_all = (K + BK - 1) / BK;
+  const int sp = SPLIT ? (int)blockIdx.y : 0, S = SPLIT ? (int)gridDim.y : 1;
+  const int c_beg = SPLIT ? nk_all * sp / S : 0, c_end = SPLIT ? nk_all * (sp + 1) / S : nk_all;
+  const int kbeg = c_beg * BK;
+  const int kend = SPLIT ? min(K, c_end * BK) : K;     // A reads stop here
+  const int kbend = SPLIT ? min(Kp, c_end * BK) : Kp;  // B reads stop here
 
   // ---- per-thread A rows (fixed across K chunks)
   const int kq = tid & 7;  // float4 index inside the 32-wide K chunk
@@ -192,13 +201,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   uint4 rbh[2][B_LD], rbl[2][B_LD];
   // scalar tap walk (MODE 1): the chunk at k0 reads channels ci0 .. ci0+31 of tap (kh, kw)
   int t_tap = 0, t_ci = 0, t_kw = 0, t_off = 0;
+  if (SPLIT && MODE == 1) {  // the walk's state at this slice's first chunk (slices start on chunk boundaries)
+    t_tap = kbeg / a.Cin;
+    t_ci = kbeg - t_tap * a.Cin;
+    t_kw = t_tap % a.KW;
+    t_off = (t_tap / a.KW) * in_sh + t_kw * in_sw + t_ci;
+  }
 
   auto load_chunk = [&](auto SET, int k0) {
     constexpr int S = decltype(SET)::value;
     if constexpr (MODE == 1) {
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
-        const bool ok = t_tap < 32 && ((amask[i] >> (t_tap & 31)) & 1u);
+        const bool ok = t_tap < 32 && ((amask[i] >> (t_tap & 31)) & 1u) && (!SPLIT || k0 < kend);
         const uint32_t off = ok ? (uint32_t)(abase[i] + t_off) * 4u : kOOB;
         uint4 u = bload16(rin, off);
         ra[S][i] = *reinterpret_cast<float4*>(&u);
@@ -217,7 +232,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
       }
     } else {
       const int kk = k0 + kq * 4;
-      const bool kv = kk < K;
+      const bool kv = kk < kend;
       const int tap = kk / a.Cin;
       const int ci = kk - tap * a.Cin;
       const int kh = tap / a.KW;
@@ -234,7 +249,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
       const int kb = k0 + ((tid + NT * j) & 3) * 8;
-      const uint32_t off = (bok[j] && kb < Kp) ? boff[j] + (uint32_t)k0 * 2u : kOOB;
+      const uint32_t off = (bok[j] && kb < kbend) ? boff[j] + (uint32_t)k0 * 2u : kOOB;
       rbh[S][j] = bload16(rwh, off);
       if constexpr (PREC == 0) rbl[S][j] = bload16(rwl, off);
     }
@@ -317,7 +332,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
     }
   }
 
-  const int nk = (K + BK - 1) / BK;
+  const int nk = c_end - c_beg;
   const std::integral_constant<int, 0> I0;
   const std::integral_constant<int, 1> I1;
 
@@ -388,20 +403,35 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   auto iteration = [&](int kc, auto NEXT) {
     compute(kc & 1);
     store_chunk((kc + 1) & 1, NEXT);
-    load_chunk(NEXT, (kc + 3) * BK);
+    load_chunk(NEXT, kbeg + (kc + 3) * BK);
     __syncthreads();
   };
 
-  load_chunk(I0, 0);
-  load_chunk(I1, BK);
+  load_chunk(I0, kbeg);
+  load_chunk(I1, kbeg + BK);
   store_chunk(0, I0);
-  load_chunk(I0, 2 * BK);
+  load_chunk(I0, kbeg + 2 * BK);
   __syncthreads();
   for (int kc = 0; kc < nk; kc += 2) {
     iteration(kc, I1);
     iteration(kc + 1, I0);
   }
 
+  if constexpr (SPLIT) {
+    // raw partial accumulators, C layout: lanes 0-31 of a register hold 32 consecutive channels of one row
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + (wn * TN + j) * 32 + li;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (m < M && n < a.Cout) a.split_part[((int64_t)sp * M + m) * a.Cout + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
   // ---- epilogue: 16-B quads through LDS when every row is 16-B aligned, else per accumulator element
   bool bad = false;
   if (epi_quads_ok(a)) {
@@ -492,6 +522,67 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
   DD_HIP_CHECK(hipGetLastError());
 }
 
+// the K-split partials summed in split order, then conv_x3's epilogue (scale, bias, residual, ReLU, strided NHWC out)
+__global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M, int S) {
+  const int QN = a.Cout / 4;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)M * QN) return;
+  const int m = (int)(e / QN), nq = 4 * (int)(e - (int64_t)m * QN);
+  float4 s = *reinterpret_cast<const float4*>(a.split_part + (int64_t)m * a.Cout + nq);
+  for (int sp = 1; sp < S; ++sp) {
+    const float4 p = *reinterpret_cast<const float4*>(a.split_part + ((int64_t)sp * M + m) * a.Cout + nq);
+    s.x += p.x;
+    s.y += p.y;
+    s.z += p.z;
+    s.w += p.w;
+  }
+  const bool bad = !(__builtin_isfinite(s.x) && __builtin_isfinite(s.y) && __builtin_isfinite(s.z) &&
+                     __builtin_isfinite(s.w));
+  const int ow = m % a.Wo, t2 = m / a.Wo, oh = t2 % a.Ho, n = t2 / a.Ho;
+  const float sc[4] = {a.wsinv[nq] * a.alpha, a.wsinv[nq + 1] * a.alpha, a.wsinv[nq + 2] * a.alpha,
+                       a.wsinv[nq + 3] * a.alpha};
+  float b[4] = {0.f, 0.f, 0.f, 0.f}, r[4] = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias)
+    for (int k = 0; k < 4; ++k) b[k] = a.bias[nq + k];
+  if (a.res) {
+    const float* rr = a.res + n * a.res_sn + oh * a.res_sh + ow * a.res_sw + nq;
+    for (int k = 0; k < 4; ++k) r[k] = rr[k];
+  }
+  const float sv[4] = {s.x, s.y, s.z, s.w};
+  float* o = a.out + n * a.out_sn + oh * a.out_sh + ow * a.out_sw + nq;
+  for (int k = 0; k < 4; ++k) {
+    float v = sv[k] * sc[k] + b[k] + r[k];
+    if (a.relu) v = fmaxf(v, 0.f);
+    o[k] = v;
+  }
+  if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+}
+
+// K-split conv_x3 (64 x 64 tiles, f16x3, the MODE-1 tap walk) for grids far below the chip: S splits of the K chunks,
+// then the reduce launch. The latency of one workgroup's whole K loop (LiDAR layer 4 at batch 1: 8 workgroups,
+// K = 4608, 61-75 us) becomes S shorter loops side by side.
+static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st) {
+  const char* se = getenv("DDMI_X3_SPLIT");  // read per dispatch; 1: on (being validated), 0 / unset: off
+  if (!se || !atoi(se)) return false;
+  if (!a.split_part || a.prec != 0 || a.rowmap || a.Cin % BK || a.KH * a.KW > 32 || a.Cout % 4) return false;
+  const int64_t tiles = (int64_t)((M + 63) / 64) * ((a.Cout + 63) / 64);
+  const int nk = (K + BK - 1) / BK;
+  if (tiles >= 64 || nk < 32) return false;
+  int S = 1;
+  while (S < 8 && tiles * S * 2 <= 128 && nk / (S * 2) >= 8) S *= 2;
+  if (S < 2 || (int64_t)S * M * a.Cout > a.split_cap) return false;
+  const int ntm = (M + 63) / 64, ntn = (a.Cout + 63) / 64;
+  static const std::string name = "conv_x3<64,64,f16x3,ksplit>";
+  set_last_conv_config(name.c_str());
+  hipLaunchKernelGGL((conv_x3_kernel<2, 2, 1, 1, 1, 0, 0, 1>), dim3(ntm * ntn, S), dim3(256), 0, st, a, M, K, ntm,
+                     ntn);
+  DD_HIP_CHECK(hipGetLastError());
+  const int64_t quads = (int64_t)M * (a.Cout / 4);
+  hipLaunchKernelGGL(x3_split_reduce, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, st, a, M, S);
+  DD_HIP_CHECK(hipGetLastError());
+  return true;
+}
+
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st);  // conv_x5.hip
 bool launch_conv_x6(const ConvArgs& a, hipStream_t st);                 // conv_x6.hip
 
@@ -566,6 +657,7 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
     return;
   }
   g_last_conv = "conv_x3";
+  if (launch_x3_split(a0, M, K, st)) return;
   const int64_t t128 = ((M + 127) / 128) * (int64_t)((a0.Cout + 127) / 128);
   const bool generic = !(a0.Cin % BK == 0 && a0.KH * a0.KW <= 32);
   if (a0.Cout <= 64) {

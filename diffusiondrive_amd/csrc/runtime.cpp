@@ -1023,8 +1023,14 @@ class Model {
     DD_HIP_CHECK(hipEventRecord(e, st_side));
     DD_HIP_CHECK(hipStreamWaitEvent(st_main, e, 0));
   }
+  bool in_side = false;  // inside side(f): per-stream scratch (conv_x3's K-split partials) takes the side's copy
   template <class F>
   void side(F&& f) {
+    struct SideFlag {
+      bool& b;
+      explicit SideFlag(bool& x) : b(x) { b = true; }
+      ~SideFlag() { b = false; }
+    } flag(in_side);
     if (seg_cap) {  // launches stay on st_cap; the segment is tagged with the side stream
       seg_end();
       seg_begin(1);
@@ -1207,6 +1213,12 @@ class Model {
             int64_t rsh = 0, int64_t rsw = 0) {
     ConvArgs a = conv_args(c, in, isn, ish, isw, N, H, Wd, out, osn, osh, osw, relu, res, rsn, rsh, rsw);
     const double fl = 2.0 * N * a.Ho * a.Wo * (double)c.cout * c.k * c.k * c.cin_real;
+    // small outputs (batch-1-sized maps): K-split scratch for conv_x3, one per stream of the forward
+    const int64_t mo = (int64_t)N * a.Ho * a.Wo * c.cout;
+    if (a.wh && a.prec == 0 && mo <= (int64_t(1) << 20)) {
+      a.split_cap = 8 * mo;
+      a.split_part = buf(in_side ? "x3_split_side" : "x3_split_main", (size_t)a.split_cap);
+    }
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
     pool_done = a.pool_out && last_conv_pooled();
   }
