@@ -562,8 +562,8 @@ __global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M, int S)
 // then the reduce launch. The latency of one workgroup's whole K loop (LiDAR layer 4 at batch 1: 8 workgroups,
 // K = 4608, 61-75 us) becomes S shorter loops side by side.
 static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st) {
-  const char* se = getenv("DDMI_X3_SPLIT");  // read per dispatch; 1: on (being validated), 0 / unset: off
-  if (!se || !atoi(se)) return false;
+  const char* se = getenv("DDMI_X3_SPLIT");  // read per dispatch; 0: off
+  if (se && !atoi(se)) return false;
   if (!a.split_part || a.prec != 0 || a.rowmap || a.Cin % BK || a.KH * a.KW > 32 || a.Cout % 4) return false;
   const int64_t tiles = (int64_t)((M + 63) / 64) * ((a.Cout + 63) / 64);
   const int nk = (K + BK - 1) / BK;

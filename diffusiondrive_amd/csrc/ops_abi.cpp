@@ -174,8 +174,18 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
     a.wsinv = ar.ptr(x.sinv);
     a.ldh = x.ldh;
     a.flags = flags;
+    // K-split scratch, as the forward provides it (runtime.cpp: conv): small grids may take conv_x3's split form
+    const int64_t mo = (int64_t)B * a.Ho * a.Wo * Cout;
+    float* part = nullptr;
+    if (prec == 0 && mo <= (1 << 20)) {
+      DD_HIP_CHECK(hipMalloc(&part, (size_t)(8 * mo) * sizeof(float)));
+      a.split_part = part;
+      a.split_cap = 8 * mo;
+    }
     launch_conv_gemm(a, S(stream));
-    DD_HIP_CHECK(hipStreamSynchronize(S(stream)));  // the split images die with `ar`
+    const hipError_t e = hipStreamSynchronize(S(stream));  // the split images die with `ar`
+    if (part) DD_HIP_CHECK(hipFree(part));
+    DD_HIP_CHECK(e);
   });
 }
 

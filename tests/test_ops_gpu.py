@@ -139,7 +139,7 @@ def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     (1, 160, 128, 128, 384, 1, 1, 0, False, False, "conv_x5<256,128>"),      # GPT qkv at C = 128
     (1, 160, 128, 256, 256, 1, 1, 0, False, True, "conv_x3<64,64,f16x3>"),   # GPT proj at C = 256 (80 tiles)
     (64, 8, 8, 512, 512, 3, 1, 1, True, True, "conv_x6<8,8,128,2,4>"),       # LiDAR layer4 (8 x 8 maps)
-    (2, 8, 8, 512, 512, 3, 1, 1, True, True, "conv_x3<64,64,f16x3>"),        # too few 8 x 8 tiles for conv_x6
+    (2, 8, 8, 512, 512, 3, 1, 1, True, True, "conv_x3<64,64,f16x3,ksplit>"), # too few 8 x 8 tiles for conv_x6
 ])
 def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, route):
     """f16x3 conv at the B = 64 forward's shapes: the dispatcher must take the named kernel / tile
@@ -232,6 +232,45 @@ def test_conv2d_small_grid_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin,
     if prec == 0:
         ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), 1, 1) + r.double())
         close(small.permute(0, 3, 1, 2), ref, 3e-5)
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s", [
+    (1, 8, 8, 512, 512, 3, 1),    # LiDAR layer-4 3x3 at batch 1 (8 tiles, K = 4608: 8 splits)
+    (2, 8, 8, 512, 512, 3, 1),    # 16 tiles: 4 splits
+    (1, 8, 8, 256, 512, 3, 2),    # layer-4 entry 3x3 / s2 (2 tiles of M = 16)
+    (1, 8, 8, 2048, 512, 1, 1),   # 1x1, K = 2048: 8 splits
+    (1, 5, 7, 1056, 200, 1, 1),   # ragged M, N (Cout % 64 != 0) and K chunks (33 over 4 splits)
+])
+def test_conv_x3_k_split(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
+    """conv_x3's K-split form for grids far below the chip (default; DDMI_X3_SPLIT=0 disables, read per dispatch):
+    S workgroups per tile over disjoint K-chunk ranges, partials summed in split order by the reduce launch, which
+    applies bias / residual / ReLU. A different summation order from the one-workgroup form, so the bar is the f16x3
+    one against fp64 (both forms), and the split output is the same on every run."""
+    p = k // 2
+    x = rnd(B, Cin, H, W, seed=91)
+    w = rnd(Cout, Cin, k, k, seed=92, scale=1.0 / np.sqrt(Cin * k * k))
+    b = rnd(Cout, seed=93)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    r = rnd(B, Cout, Ho, Wo, seed=94)
+    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
+
+    def run(split):
+        monkeypatch.setenv("DDMI_X3_SPLIT", split)
+        out = torch.full((B, Ho, Wo, Cout), float("nan"), device=DEV)
+        flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
+                               out.data_ptr(), Cout, k, k, s, p, 1, 0, flags.data_ptr(), None), gpu)
+        assert int(flags.item()) == 0
+        return out, gpu.dd_op_last_kernel().decode()
+
+    sp, route = run("1")
+    sp2, _ = run("1")
+    base, route0 = run("0")
+    assert route == "conv_x3<64,64,f16x3,ksplit>" and route0 != route, (route, route0)
+    assert torch.equal(sp, sp2)
+    ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), s, p) + r.double())
+    close(sp.permute(0, 3, 1, 2), ref, 3e-5)
+    close(base.permute(0, 3, 1, 2), ref, 3e-5)
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,s", [
