@@ -561,15 +561,18 @@ __global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M, int S)
 // K-split conv_x3 (64 x 64 tiles, f16x3, the MODE-1 tap walk) for grids far below the chip: S splits of the K chunks,
 // then the reduce launch. The latency of one workgroup's whole K loop (LiDAR layer 4 at batch 1: 8 workgroups,
 // K = 4608, 61-75 us) becomes S shorter loops side by side.
-static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st) {
-  const char* se = getenv("DDMI_X3_SPLIT");  // read per dispatch; 0: off
-  if (se && !atoi(se)) return false;
+static int x3_split_mode() {
+  const char* se = getenv("DDMI_X3_SPLIT");  // read per dispatch; 0: off, 2: also ahead of conv_x6 (256 workgroups)
+  return se ? atoi(se) : 1;
+}
+static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st, int wg_target = 128) {
+  if (!x3_split_mode()) return false;
   if (!a.split_part || a.prec != 0 || a.rowmap || a.Cin % BK || a.KH * a.KW > 32 || a.Cout % 4) return false;
   const int64_t tiles = (int64_t)((M + 63) / 64) * ((a.Cout + 63) / 64);
   const int nk = (K + BK - 1) / BK;
   if (tiles >= 64 || nk < 32) return false;
   int S = 1;
-  while (S < 8 && tiles * S * 2 <= 128 && nk / (S * 2) >= 8) S *= 2;
+  while (S < 8 && tiles * S * 2 <= wg_target && nk / (S * 2) >= 8) S *= 2;
   if (S < 2 || (int64_t)S * M * a.Cout > a.split_cap) return false;
   const int ntm = (M + 63) / 64, ntn = (a.Cout + 63) / 64;
   static const std::string name = "conv_x3<64,64,f16x3,ksplit>";
@@ -646,6 +649,10 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t st) {
   if (a0.rowmap) {
     g_last_conv = "conv_x3";
     launch_x3_cfg<2, 2, 2, 2, 1>(a0, M, K, st);  // gathered rows: 128 x 128
+    return;
+  }
+  if (x3_split_mode() == 2 && launch_x3_split(a0, M, K, st, 256)) {
+    g_last_conv = "conv_x3";
     return;
   }
   if (launch_conv_x6(a0, st)) {
