@@ -562,8 +562,10 @@ __global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M, int S)
 // then the reduce launch. The latency of one workgroup's whole K loop (LiDAR layer 4 at batch 1: 8 workgroups,
 // K = 4608, 61-75 us) becomes S shorter loops side by side.
 static int x3_split_mode() {
-  const char* se = getenv("DDMI_X3_SPLIT");  // read per dispatch; 0: off, 2: also ahead of conv_x6 (256 workgroups)
-  return se ? atoi(se) : 1;
+  // read per dispatch; 2 (default): the split ahead of conv_x6 with up to 256 workgroups, 1: only where conv_x6 /
+  // conv_x5 decline (up to 128), 0: off
+  const char* se = getenv("DDMI_X3_SPLIT");
+  return se ? atoi(se) : 2;
 }
 static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st, int wg_target = 128) {
   if (!x3_split_mode()) return false;

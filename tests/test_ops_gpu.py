@@ -216,6 +216,8 @@ def test_conv2d_small_grid_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin,
     r = rnd(B, Cout, H, W, seed=78)
     xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
 
+    monkeypatch.setenv("DDMI_X3_SPLIT", "1")  # conv_x6's forms, not conv_x3's K split ahead of them
+
     def run(small):
         monkeypatch.setenv("DDMI_X6_SMALL", small)
         out = torch.empty(B, H, W, Cout, device=DEV)
@@ -240,9 +242,12 @@ def test_conv2d_small_grid_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin,
     (1, 8, 8, 256, 512, 3, 2),    # layer-4 entry 3x3 / s2 (2 tiles of M = 16)
     (1, 8, 8, 2048, 512, 1, 1),   # 1x1, K = 2048: 8 splits
     (1, 5, 7, 1056, 200, 1, 1),   # ragged M, N (Cout % 64 != 0) and K chunks (33 over 4 splits)
+    (1, 8, 32, 512, 512, 3, 1),   # image layer 4 at batch 1: ahead of conv_x6 (32 tiles, 4 splits)
+    (1, 16, 16, 256, 256, 3, 1),  # LiDAR layer 3 at batch 1 (16 tiles, 4 splits)
 ])
 def test_conv_x3_k_split(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
-    """conv_x3's K-split form for grids far below the chip (default; DDMI_X3_SPLIT=0 disables, read per dispatch):
+    """conv_x3's K-split form for grids far below the chip (default DDMI_X3_SPLIT=2, ahead of conv_x6; 0 disables;
+    read per dispatch):
     S workgroups per tile over disjoint K-chunk ranges, partials summed in split order by the reduce launch, which
     applies bias / residual / ReLU. A different summation order from the one-workgroup form, so the bar is the f16x3
     one against fp64 (both forms), and the split output is the same on every run."""
@@ -263,8 +268,8 @@ def test_conv_x3_k_split(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
         assert int(flags.item()) == 0
         return out, gpu.dd_op_last_kernel().decode()
 
-    sp, route = run("1")
-    sp2, _ = run("1")
+    sp, route = run("2")
+    sp2, _ = run("2")
     base, route0 = run("0")
     assert route == "conv_x3<64,64,f16x3,ksplit>" and route0 != route, (route, route0)
     assert torch.equal(sp, sp2)
