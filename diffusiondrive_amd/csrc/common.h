@@ -66,6 +66,9 @@ struct ConvArgs {
   // partials, summed in split order by a reduce launch that applies the epilogue; null: no split
   float* split_part = nullptr;
   int64_t split_cap = 0;  // floats
+  // per-tile arrival counters (>= 64, zeroed once, self-resetting): the last split of a tile sums the partials and
+  // applies the epilogue itself (no reduce launch); null: the reduce launch
+  unsigned* split_cnt = nullptr;
   int batch = 1, zdiv = 1;
   int64_t in_z1 = 0, in_z2 = 0, w_z1 = 0, w_z2 = 0, out_z1 = 0, out_z2 = 0, res_z1 = 0, res_z2 = 0;
   int64_t flops_K = -1;  // algorithmic K per output (excluding channel padding); -1 = KH*KW*Cin

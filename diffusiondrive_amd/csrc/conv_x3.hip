@@ -418,6 +418,68 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   }
 
   if constexpr (SPLIT) {
+    if (a.split_cnt) {
+      // fused hand-off (value_proj.hip's form): partials stored write-through (sc1), drained, one agent-scope add per
+      // workgroup on the tile's counter; the last adder resets it, loads the other splits' partials (sc1) and sums
+      // all S in split order - the reduce launch's order and epilogue expressions
+      __shared__ int s_last;
+      const __amdgpu_buffer_rsrc_t rp = make_rsrc(a.split_part);
+      auto poff = [&](int s2, int m, int n) { return (uint32_t)((((int64_t)s2 * M + m) * a.Cout + n) * 4); };
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + (wn * TN + j) * 32 + li;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const float v = acc[i][j][r];  // (a bit_cast of the vector-element lvalue itself reads element 0)
+            if (m < M && n < a.Cout)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rp, poff(sp, m, n), 0, 16);
+          }
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(a.split_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (unsigned)(S - 1);
+        if (old == (unsigned)(S - 1)) {
+          __hip_atomic_store(a.split_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      __syncthreads();
+      if (!s_last) return;
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + (wn * TN + j) * 32 + li;
+          if (n >= a.Cout) continue;
+          const float sc = a.wsinv[n] * a.alpha, bv = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (m >= M) continue;
+            const float own = acc[i][j][r];
+            float sum = sp == 0 ? own : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, poff(0, m, n), 0, 16));
+            for (int s2 = 1; s2 < S; ++s2)
+              sum += s2 == sp ? own : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, poff(s2, m, n), 0, 16));
+            bad |= !__builtin_isfinite(sum);
+            const int ow = m % a.Wo, t2 = m / a.Wo, oh = t2 % a.Ho, im = t2 / a.Ho;
+            const float rv = a.res ? a.res[im * a.res_sn + oh * a.res_sh + ow * a.res_sw + n] : 0.f;
+            float v = sum * sc + bv + rv;
+            if (a.relu) v = fmaxf(v, 0.f);
+            a.out[im * a.out_sn + oh * a.out_sh + ow * a.out_sw + n] = v;
+          }
+        }
+      if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
+      return;
+    }
     // raw partial accumulators, C layout: lanes 0-31 of a register hold 32 consecutive channels of one row
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -579,9 +641,13 @@ static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st, int
   const int ntm = (M + 63) / 64, ntn = (a.Cout + 63) / 64;
   static const std::string name = "conv_x3<64,64,f16x3,ksplit>";
   set_last_conv_config(name.c_str());
-  hipLaunchKernelGGL((conv_x3_kernel<2, 2, 1, 1, 1, 0, 0, 1>), dim3(ntm * ntn, S), dim3(256), 0, st, a, M, K, ntm,
+  const char* fe = getenv("DDMI_X3_SPLIT_FUSE");  // read per dispatch; 1: the last split reduces (no reduce launch)
+  ConvArgs b = a;
+  if (!(fe && atoi(fe))) b.split_cnt = nullptr;
+  hipLaunchKernelGGL((conv_x3_kernel<2, 2, 1, 1, 1, 0, 0, 1>), dim3(ntm * ntn, S), dim3(256), 0, st, b, M, K, ntm,
                      ntn);
   DD_HIP_CHECK(hipGetLastError());
+  if (b.split_cnt) return true;
   const int64_t quads = (int64_t)M * (a.Cout / 4);
   hipLaunchKernelGGL(x3_split_reduce, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, st, a, M, S);
   DD_HIP_CHECK(hipGetLastError());

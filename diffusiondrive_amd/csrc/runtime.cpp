@@ -1218,6 +1218,7 @@ class Model {
     if (a.wh && a.prec == 0 && mo <= (int64_t(1) << 20)) {
       a.split_cap = 8 * mo;
       a.split_part = buf(in_side ? "x3_split_side" : "x3_split_main", (size_t)a.split_cap);
+      a.split_cnt = reinterpret_cast<unsigned*>(buf_zeroed(in_side ? "x3_split_cnt_side" : "x3_split_cnt_main", 64));
     }
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
     pool_done = a.pool_out && last_conv_pooled();

@@ -273,6 +273,13 @@ def test_conv_x3_k_split(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
     base, route0 = run("0")
     assert route == "conv_x3<64,64,f16x3,ksplit>" and route0 != route, (route, route0)
     assert torch.equal(sp, sp2)
+    # the last split of each tile reducing in-kernel (DDMI_X3_SPLIT_FUSE=1): the reduce launch's order and expressions
+    monkeypatch.setenv("DDMI_X3_SPLIT_FUSE", "1")
+    fu, _ = run("2")
+    fu2, _ = run("2")
+    monkeypatch.delenv("DDMI_X3_SPLIT_FUSE")
+    assert torch.equal(fu, fu2)
+    close(fu.permute(0, 3, 1, 2), sp.permute(0, 3, 1, 2).double(), 1e-6)
     ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), s, p) + r.double())
     close(sp.permute(0, 3, 1, 2), ref, 3e-5)
     close(base.permute(0, 3, 1, 2), ref, 3e-5)
