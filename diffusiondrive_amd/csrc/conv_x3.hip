@@ -466,9 +466,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
             const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
             if (m >= M) continue;
             const float own = acc[i][j][r];
-            float sum = sp == 0 ? own : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, poff(0, m, n), 0, 16));
-            for (int s2 = 1; s2 < S; ++s2)
-              sum += s2 == sp ? own : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, poff(s2, m, n), 0, 16));
+            // all (up to 8) splits' loads issued before the ordered sum (unconditional: past S reads the OOB zero)
+            float p[8];
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2)
+              p[s2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    rp, s2 < S && s2 != sp ? poff(s2, m, n) : kOOB, 0, 16));
+            float sum = sp == 0 ? own : p[0];
+#pragma unroll
+            for (int s2 = 1; s2 < 8; ++s2)
+              if (s2 < S) sum += s2 == sp ? own : p[s2];
             bad |= !__builtin_isfinite(sum);
             const int ow = m % a.Wo, t2 = m / a.Wo, oh = t2 % a.Ho, im = t2 / a.Ho;
             const float rv = a.res ? a.res[im * a.res_sn + oh * a.res_sh + ow * a.res_sw + n] : 0.f;
