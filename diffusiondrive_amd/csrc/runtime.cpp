@@ -1218,7 +1218,9 @@ class Model {
     if (a.wh && a.prec == 0 && mo <= (int64_t(1) << 20)) {
       a.split_cap = 8 * mo;
       a.split_part = buf(in_side ? "x3_split_side" : "x3_split_main", (size_t)a.split_cap);
-      a.split_cnt = reinterpret_cast<unsigned*>(buf_zeroed(in_side ? "x3_split_cnt_side" : "x3_split_cnt_main", 64));
+      const char* fe = getenv("DDMI_X3_SPLIT_FUSE");  // opt-in in-kernel split reduce (measured slower: round5_ab.md)
+      if (fe && atoi(fe))
+        a.split_cnt = reinterpret_cast<unsigned*>(buf_zeroed(in_side ? "x3_split_cnt_side" : "x3_split_cnt_main", 64));
     }
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
     pool_done = a.pool_out && last_conv_pooled();
