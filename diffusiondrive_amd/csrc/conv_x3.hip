@@ -592,18 +592,37 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 }
 
 // the K-split partials summed in split order, then conv_x3's epilogue (scale, bias, residual, ReLU, strided NHWC out)
-__global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M, int S) {
+// (SS = S as a template parameter: every split's load is issued before the ordered sum; SS = 0: a runtime-S loop,
+// DDMI_X3_RED_LOOP=1, same order and result)
+template <int SS>
+__global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M, int S_rt) {
   const int QN = a.Cout / 4;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)M * QN) return;
   const int m = (int)(e / QN), nq = 4 * (int)(e - (int64_t)m * QN);
-  float4 s = *reinterpret_cast<const float4*>(a.split_part + (int64_t)m * a.Cout + nq);
-  for (int sp = 1; sp < S; ++sp) {
-    const float4 p = *reinterpret_cast<const float4*>(a.split_part + ((int64_t)sp * M + m) * a.Cout + nq);
-    s.x += p.x;
-    s.y += p.y;
-    s.z += p.z;
-    s.w += p.w;
+  float4 s;
+  if constexpr (SS > 0) {
+    float4 p[SS];
+#pragma unroll
+    for (int sp = 0; sp < SS; ++sp)
+      p[sp] = *reinterpret_cast<const float4*>(a.split_part + ((int64_t)sp * M + m) * a.Cout + nq);
+    s = p[0];
+#pragma unroll
+    for (int sp = 1; sp < SS; ++sp) {
+      s.x += p[sp].x;
+      s.y += p[sp].y;
+      s.z += p[sp].z;
+      s.w += p[sp].w;
+    }
+  } else {
+    s = *reinterpret_cast<const float4*>(a.split_part + (int64_t)m * a.Cout + nq);
+    for (int sp = 1; sp < S_rt; ++sp) {
+      const float4 p = *reinterpret_cast<const float4*>(a.split_part + ((int64_t)sp * M + m) * a.Cout + nq);
+      s.x += p.x;
+      s.y += p.y;
+      s.z += p.z;
+      s.w += p.w;
+    }
   }
   const bool bad = !(__builtin_isfinite(s.x) && __builtin_isfinite(s.y) && __builtin_isfinite(s.z) &&
                      __builtin_isfinite(s.w));
@@ -656,7 +675,16 @@ static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st, int
   DD_HIP_CHECK(hipGetLastError());
   if (b.split_cnt) return true;
   const int64_t quads = (int64_t)M * (a.Cout / 4);
-  hipLaunchKernelGGL(x3_split_reduce, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, st, a, M, S);
+  const dim3 rg((unsigned)((quads + 255) / 256));
+  const char* rl = getenv("DDMI_X3_RED_LOOP");
+  if (rl && atoi(rl))
+    hipLaunchKernelGGL(x3_split_reduce<0>, rg, dim3(256), 0, st, a, M, S);
+  else if (S == 2)
+    hipLaunchKernelGGL(x3_split_reduce<2>, rg, dim3(256), 0, st, a, M, S);
+  else if (S == 4)
+    hipLaunchKernelGGL(x3_split_reduce<4>, rg, dim3(256), 0, st, a, M, S);
+  else
+    hipLaunchKernelGGL(x3_split_reduce<8>, rg, dim3(256), 0, st, a, M, S);
   DD_HIP_CHECK(hipGetLastError());
   return true;
 }

@@ -278,6 +278,10 @@ def test_conv_x3_k_split(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
     fu, _ = run("2")
     fu2, _ = run("2")
     monkeypatch.delenv("DDMI_X3_SPLIT_FUSE")
+    monkeypatch.setenv("DDMI_X3_RED_LOOP", "1")  # the runtime-S reduce loop: same order, same bits
+    lp, _ = run("2")
+    monkeypatch.delenv("DDMI_X3_RED_LOOP")
+    assert torch.equal(lp, sp)
     assert torch.equal(fu, fu2)
     close(fu.permute(0, 3, 1, 2), sp.permute(0, 3, 1, 2).double(), 1e-6)
     ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), s, p) + r.double())
