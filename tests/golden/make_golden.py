@@ -15,10 +15,16 @@ Noise is the reference's own draw: ``torch.manual_seed(seed)`` right before ``fo
 (transfuser_model_v2.py:593 is the only RNG consumer). Inputs are regenerated from the seed
 by ``synthetic_inputs`` and their checksums are stored so tests can confirm regeneration.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [B:seed ...]
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [B:seed[:r50] ...]
 Writes tests/golden/ref_b{B}_s{seed}.npz and tests/golden/state_dict_schema.json. Default cases:
 B=1 (seed 11), B=4 (seed 1234) and B=64 (seed 1234) -- the last is exactly bench.py's rank-0
 workload (``synthetic_inputs(64, 1234)``), so the benchmark batch itself is pinned.
+
+Config C4 (BASELINE.json): ``B:seed:r50`` runs the reference with
+``TransfuserConfig.image_architecture = "resnet50"`` (transfuser_config.py:17; the trunk is selected
+at transfuser_backbone.py:24-33 and the GPT widths / 1x1 channel adapters follow its feature_info,
+:66-93) on ``seeded_state_dict(TransfuserConfig(image_architecture="resnet50"), 3)`` and writes
+tests/golden/ref_r50_b{B}_s{seed}.npz. Default R50 cases: B=2 (seed 77), B=4 (seed 1234).
 Nothing of the reference's source is copied; only data (inputs/outputs) is stored.
 """
 import json
@@ -39,8 +45,11 @@ import torch  # noqa: E402
 from diffusiondrive_amd.config import TransfuserConfig  # noqa: E402
 from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs  # noqa: E402
 
-CASES = [(1, 11), (4, 1234), (64, 1234)]
+CASES = [(1, 11, "r34"), (4, 1234, "r34"), (64, 1234, "r34")]
+CASES_R50 = [(2, 77, "r50"), (4, 1234, "r50")]
 WEIGHT_SEED = 0
+WEIGHT_SEED_R50 = 3
+ARCH = {"r34": "resnet34", "r50": "resnet50"}
 MAX_SAMPLES = 4096
 
 
@@ -59,24 +68,38 @@ def main():
     from navsim.agents.diffusiondrive.transfuser_config import TransfuserConfig as RefConfig
     from navsim.agents.diffusiondrive.transfuser_model_v2 import V2TransfuserModel
 
-    cfg = TransfuserConfig()
-    sd_np = seeded_state_dict(cfg, WEIGHT_SEED)
-    with tempfile.TemporaryDirectory() as td:
-        anchor_path = os.path.join(td, "anchors.npy")
-        np.save(anchor_path, sd_np["_trajectory_head.plan_anchor"])
-        rcfg = RefConfig()
-        rcfg.plan_anchor_path = anchor_path
-        model = V2TransfuserModel(rcfg)
-    ref_sd = model.state_dict()
-    schema = [[k, list(v.shape)] for k, v in ref_sd.items()]
-    with open(os.path.join(HERE, "state_dict_schema.json"), "w") as f:
-        json.dump(schema, f, indent=0)
-    model.load_state_dict({k: torch.as_tensor(v) for k, v in sd_np.items()}, strict=True)
-    model.eval()
     torch.set_num_threads(8)
+    models = {}
 
-    cases = [tuple(int(x) for x in a.split(":")) for a in sys.argv[1:]] or CASES
-    for B, seed in cases:
+    def build(arch):
+        if arch in models:
+            return models[arch]
+        cfg = TransfuserConfig(image_architecture=ARCH[arch])
+        wseed = WEIGHT_SEED if arch == "r34" else WEIGHT_SEED_R50
+        sd_np = seeded_state_dict(cfg, wseed)
+        with tempfile.TemporaryDirectory() as td:
+            anchor_path = os.path.join(td, "anchors.npy")
+            np.save(anchor_path, sd_np["_trajectory_head.plan_anchor"])
+            rcfg = RefConfig()
+            rcfg.image_architecture = ARCH[arch]
+            rcfg.plan_anchor_path = anchor_path
+            model = V2TransfuserModel(rcfg)
+        if arch == "r34":
+            schema = [[k, list(v.shape)] for k, v in model.state_dict().items()]
+            with open(os.path.join(HERE, "state_dict_schema.json"), "w") as f:
+                json.dump(schema, f, indent=0)
+        model.load_state_dict({k: torch.as_tensor(v) for k, v in sd_np.items()}, strict=True)
+        model.eval()
+        models[arch] = (model, cfg, wseed)
+        return models[arch]
+
+    def parse(a):
+        f = a.split(":")
+        return int(f[0]), int(f[1]), (f[2] if len(f) > 2 else "r34")
+
+    cases = [parse(a) for a in sys.argv[1:]] or CASES + CASES_R50
+    for B, seed, arch in cases:
+        model, cfg, wseed = build(arch)
         inp = synthetic_inputs(B, seed, cfg)
         cap = {}
         calls = {"layer": 0, "vp": 0, "gs": 0}
@@ -128,7 +151,8 @@ def main():
         for h in hooks:
             h.remove()
 
-        rec = {"batch": np.array(B), "seed": np.array(seed), "weight_seed": np.array(WEIGHT_SEED)}
+        rec = {"batch": np.array(B), "seed": np.array(seed), "weight_seed": np.array(wseed),
+               "image_architecture": np.array(ARCH[arch])}
         for k in ("camera_feature", "lidar_feature", "status_feature", "noise"):
             a = inp[k].astype(np.float64)
             rec[f"in_{k}_sum"] = np.array(a.sum())
@@ -146,7 +170,8 @@ def main():
             else:
                 for k, v in summarize(t).items():
                     rec[f"tap_{name}_{k}"] = v
-        path = os.path.join(HERE, f"ref_b{B}_s{seed}.npz")
+        stem = "ref" if arch == "r34" else f"ref_{arch}"
+        path = os.path.join(HERE, f"{stem}_b{B}_s{seed}.npz")
         np.savez_compressed(path, **rec)
         print(f"wrote {path}: traj[0,0]={rec['trajectory'][0, 0]}, taps={sorted(cap)}")
 

@@ -19,6 +19,11 @@ def golden_files():
     return sorted(glob.glob(os.path.join(GOLDEN_DIR, "ref_b*_s*.npz")))
 
 
+def golden_files_r50():
+    """Config C4 goldens: the reference run with image_architecture="resnet50" (make_golden.py ``B:seed:r50``)."""
+    return sorted(glob.glob(os.path.join(GOLDEN_DIR, "ref_r50_b*_s*.npz")))
+
+
 def load(path):
     with np.load(path, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}

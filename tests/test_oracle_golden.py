@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from golden_util import compare_tap, golden_files, load, tap_names, waypoint_l2
+from golden_util import compare_tap, golden_files, golden_files_r50, load, tap_names, waypoint_l2
 
 
 @pytest.fixture(scope="module")
@@ -30,12 +30,35 @@ def test_inputs_regenerate(path):
     np.testing.assert_array_equal(inp["status_feature"], g["status_feature"])
 
 
+@pytest.fixture(scope="module")
+def oracle_r50():
+    """Config C4: ResNet-50 image trunk on seeded weights (seed 3), the reference's own C4 goldens."""
+    from diffusiondrive_amd.config import TransfuserConfig
+    from diffusiondrive_amd.weights import seeded_state_dict
+    from oracle.model import OracleModel
+    cfg = TransfuserConfig(image_architecture="resnet50")
+    return OracleModel(seeded_state_dict(cfg, 3), cfg)
+
+
 @pytest.mark.parametrize("path", golden_files(), ids=os.path.basename)
 def test_oracle_matches_reference(oracle, path):
+    _check_oracle(oracle, path)
+
+
+@pytest.mark.parametrize("path", golden_files_r50(), ids=os.path.basename)
+def test_oracle_resnet50_matches_reference(oracle_r50, path):
+    """C4 pinned: the oracle's Bottleneck trunk and the 256/512/1024/2048-channel fusion adapters
+    (transfuser_backbone.py:66-93) against the reference run with image_architecture="resnet50"."""
+    g = load(path)
+    assert str(g["image_architecture"]) == "resnet50" and int(g["weight_seed"]) == 3
+    _check_oracle(oracle_r50, path)
+
+
+def _check_oracle(oracle, path):
     from oracle.model import Taps
     from diffusiondrive_amd.weights import synthetic_inputs
     g = load(path)
-    inp = synthetic_inputs(int(g["batch"]), int(g["seed"]))
+    inp = synthetic_inputs(int(g["batch"]), int(g["seed"]), oracle.cfg)
     taps = Taps()
     out = oracle.forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"], inp["noise"], taps=taps)
     assert waypoint_l2(out["trajectory"].numpy(), g["trajectory"]) <= 2e-5

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import compare_tap, golden_files, load, waypoint_l2
+from golden_util import compare_tap, golden_files, golden_files_r50, load, waypoint_l2
 
 pytestmark = pytest.mark.gpu
 
@@ -45,14 +45,20 @@ GEMM_MODES = ["fp32", "f16x3"]
 @pytest.mark.parametrize("mode", GEMM_MODES)
 @pytest.mark.parametrize("path", golden_files(), ids=os.path.basename)
 def test_forward_matches_reference_goldens(gpu_model, path, mode):
+    _check_golden(gpu_model, path, mode)
+
+
+def _check_golden(model, path, mode, cfg=None):
+    """Run the golden's batch through ``model`` in ``mode`` and hold the trajectory, every per-(step, layer)
+    poses_reg / poses_cls, the agent outputs and the intermediates to the bars above."""
     from diffusiondrive_amd.weights import synthetic_inputs
-    gpu_model.set_gemm_mode(mode)
+    model.set_gemm_mode(mode)
     g = load(path)
     B, seed = int(g["batch"]), int(g["seed"])
-    inp = synthetic_inputs(B, seed)
+    inp = synthetic_inputs(B, seed, cfg)
     assert np.array_equal(inp["noise"], g["noise"])
     feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
-    out = gpu_model.forward(feats, noise=torch.from_numpy(inp["noise"]), heads=True, modes=True)
+    out = model.forward(feats, noise=torch.from_numpy(inp["noise"]), heads=True, modes=True)
     lines = [f"== {os.path.basename(path)} B={B} gemm={mode}"]
     l2 = waypoint_l2(out["trajectory"].numpy(), g["trajectory"])
     hd = float(np.abs(out["trajectory"].numpy()[..., 2] - g["trajectory"][..., 2]).max())
@@ -60,33 +66,35 @@ def test_forward_matches_reference_goldens(gpu_model, path, mode):
     errs = {}
     for s in range(2):
         for l in range(2):
-            reg = gpu_model.tap(f"reg_s{s}l{l}", (B, 20, 8, 3)).cpu().numpy()
-            cls = gpu_model.tap(f"cls_s{s}l{l}", (B, 20)).cpu().numpy()
+            reg = model.tap(f"reg_s{s}l{l}", (B, 20, 8, 3)).cpu().numpy()
+            cls = model.tap(f"cls_s{s}l{l}", (B, 20)).cpu().numpy()
             errs[f"reg_s{s}l{l}"] = float(np.abs(reg - g[f"reg_s{s}l{l}"]).max())
             errs[f"cls_s{s}l{l}"] = float(np.abs(cls - g[f"cls_s{s}l{l}"]).max())
     errs["agent_states"] = float(np.abs(out["agent_states"].numpy() - g["agent_states"]).max())
     errs["agent_labels"] = float(np.abs(out["agent_labels"].numpy() - g["agent_labels"]).max())
+    c4 = int(g["tap_img_l4_shape"][1])   # 512 (ResNet-34) / 2048 (ResNet-50)
     taps = {
-        "p3": _nchw(gpu_model.tap("cross_in"), B, 64, 64, 320)[:, 256:],
-        "bev_feature": _nchw(gpu_model.tap("bev_feature"), B, 8, 8, 512),
-        "keyval": gpu_model.tap("keyval", (B, 65, 256)),
-        "cross_bev_tokens": gpu_model.tap("cross_bev", (B, 4096, 256)),
-        "query_out": gpu_model.tap("query_out", (B, 31, 256)),
+        "img_l4": _nchw(model.tap("img_l4"), B, 8, 32, c4),
+        "p3": _nchw(model.tap("cross_in"), B, 64, 64, 320)[:, 256:],
+        "bev_feature": _nchw(model.tap("bev_feature"), B, 8, 8, 512),
+        "keyval": model.tap("keyval", (B, 65, 256)),
+        "cross_bev_tokens": model.tap("cross_bev", (B, 4096, 256)),
+        "query_out": model.tap("query_out", (B, 31, 256)),
         "bev_semantic_map": out["bev_semantic_map"],
     }
     for s in range(2):
         for l in range(2):
-            taps[f"gs_s{s}l{l}"] = gpu_model.tap(f"gs_s{s}l{l}", (B, 20, 256))
+            taps[f"gs_s{s}l{l}"] = model.tap(f"gs_s{s}l{l}", (B, 20, 256))
     if mode != "f16x3":  # f16x3 evaluates value_proj only at the sampled taps (test below)
         for l in range(2):
-            taps[f"value_call{l}_l{l}"] = _nchw(gpu_model.tap(f"value_l{l}"), B, 64, 64, 256)
+            taps[f"value_call{l}_l{l}"] = _nchw(model.tap(f"value_l{l}"), B, 64, 64, 256)
     tap_errs = {k: compare_tap(g, k, v.cpu().numpy()) for k, v in taps.items()}
     for k, v in errs.items():
         lines.append(f"  {k:22s} max abs err {v:.3e}")
     for k, (e, cs) in tap_errs.items():
         lines.append(f"  tap {k:18s} sample rel err {e:.3e}  checksum rel err {cs:.3e}")
     _report(lines)
-    assert gpu_model.numerics_flags() == 0
+    assert model.numerics_flags() == 0
     assert l2 <= WAYPOINT_L2_TOL, f"waypoint L2 {l2:.3e} > {WAYPOINT_L2_TOL}"
     assert hd <= HEADING_TOL
     for k, v in errs.items():
@@ -127,29 +135,25 @@ def test_forward_matches_oracle_batch8(gpu_model, seeded_sd, mode):
     assert l2 <= WAYPOINT_L2_TOL
 
 
-@pytest.mark.parametrize("mode", GEMM_MODES)
-def test_resnet50_config_matches_oracle(mode):
-    """BASELINE config C4: ResNet-50 image trunk (TransfuserConfig.image_architecture="resnet50",
-    LiDAR stays ResNet-34, channels adapt via transfuser_backbone.py:67-93) vs the CPU oracle.
-    Parity here is pinned through the oracle (its ResNet-34 path is golden-pinned; the ResNet-50
-    Bottleneck restatement shares every primitive)."""
+@pytest.fixture(scope="module")
+def r50_model(gpu):
     from diffusiondrive_amd.config import TransfuserConfig
     from diffusiondrive_amd.model import DiffusionDriveModel
-    from diffusiondrive_amd.weights import seeded_state_dict, synthetic_inputs
-    from oracle.model import OracleModel
+    from diffusiondrive_amd.weights import seeded_state_dict
     cfg = TransfuserConfig(image_architecture="resnet50")
-    sd = seeded_state_dict(cfg, 3)
-    inp = synthetic_inputs(2, 77, cfg)
-    ref = OracleModel(sd, cfg).forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"],
-                                       inp["noise"], heads=False)
-    m = DiffusionDriveModel(cfg, sd, device=0)
-    m.set_gemm_mode(mode)
-    feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
-    out = m.forward(feats, noise=torch.from_numpy(inp["noise"]))
-    l2 = waypoint_l2(out["trajectory"].numpy(), ref["trajectory"].numpy())
-    _report([f"== resnet50 B=2 gemm={mode}: waypoint L2 vs oracle {l2:.3e}"])
-    assert m.numerics_flags() == 0
-    assert l2 <= WAYPOINT_L2_TOL
+    return DiffusionDriveModel(cfg, seeded_state_dict(cfg, 3), device=0), cfg
+
+
+@pytest.mark.parametrize("mode", GEMM_MODES)
+@pytest.mark.parametrize("path", golden_files_r50(), ids=os.path.basename)
+def test_resnet50_config_matches_oracle(r50_model, path, mode):
+    """BASELINE config C4: ResNet-50 image trunk (TransfuserConfig.image_architecture="resnet50",
+    transfuser_config.py:17; LiDAR stays ResNet-34, channels adapt via transfuser_backbone.py:66-93) against
+    the REFERENCE's own C4 goldens (make_golden.py ``B:seed:r50``, B = 2 and 4; the oracle is pinned to the
+    same files in test_oracle_golden.py): trajectory, every per-(step, layer) reg / cls, the Bottleneck
+    trunk's layer-4 output and the downstream taps at the bars of the ResNet-34 goldens."""
+    m, cfg = r50_model
+    _check_golden(m, path, mode, cfg)
 
 
 @pytest.mark.parametrize("mode", GEMM_MODES)
