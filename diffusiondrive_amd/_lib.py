@@ -68,6 +68,7 @@ _SIGS = {
     "dd_get_streams": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "dd_graph_info": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                      ctypes.POINTER(ctypes.c_int)]),
+    "dd_graph_nodes": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "dd_forward_train": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         ctypes.c_int, ctypes.c_float, ctypes.c_float, c_void_p, c_void_p]),
     "dd_bev_semantic_loss": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -112,6 +112,10 @@ struct ConvArgs {
 };
 constexpr unsigned DD_NUM_F16_OVERFLOW = 1u;  // an activation |x| >= 65504 met the f16x3 split
 constexpr unsigned DD_NUM_SYNC_TIMEOUT = 2u;  // a megakernel's inter-workgroup wait gave up (tfdec_mk groups)
+// a megakernel's inter-workgroup counter held a value no healthy launch leaves there (an arrival saw more or fewer
+// earlier arrivals than its barrier allows): the waits it guards cannot be trusted; dd_numerics_flags' clear re-zeroes
+// the counters
+constexpr unsigned DD_NUM_SYNC_STATE = 4u;
 
 #ifdef __HIPCC__
 // Implicit-GEMM epilogue row table: element offsets of output / residual row m0 + r (r < BM) of a tile,

@@ -70,10 +70,11 @@ struct MkArgs {
   unsigned long long* stamps = nullptr;  // diagnostics: [B][32] shader-clock stamps per phase, or nullptr
   // query groups per scene (1, 2, 4): G workgroups of 20 / G queries each; the scene's last arriving group runs the
   // mode selection and the next taps' dedup (scene_cnt [B] zero between launches; next_pts [B][Q*P][2] carries the
-  // DDIM-updated next points of a step's layer 1)
+  // DDIM-updated next points of a step's layer 1; cls_x [B][32] the scene's cls logits on 128-B lines of its own)
   int groups = 1;
   unsigned* scene_cnt = nullptr;
   float* next_pts = nullptr;
+  float* cls_x = nullptr;
 };
 
 struct MkInitArgs {
@@ -121,14 +122,20 @@ struct TfMkArgs {
   float* ego[2] = {nullptr, nullptr};  // [B][256]
   int B = 0;
   // groups = 4: four workgroups per scene (heads / hidden chunks split over them, exchanges through xbuf):
-  // xbuf [B][9][4][32][256] floats (one buffer per exchange), sync_cnt [2B] (arrivals, finishes) zeroed at allocation
+  // xbuf [B][9][4][32][256] floats (one buffer per exchange; tfdec_mk_xbuf_floats(B)), sync_cnt [2B] (arrivals,
+  // finishes) zeroed at allocation; both capacities are checked at launch
   int groups = 1;
   float* xbuf = nullptr;
+  size_t xbuf_floats = 0;
   unsigned* sync_cnt = nullptr;
+  size_t sync_cnt_n = 0;
+  int no_reset = 0;  // diagnostics only (DDMI_TF_MEMSET=3, DDMI_TF_NORESET): the counters are left as they are
+  unsigned spin_limit = 1u << 22;  // polls before a wait gives up (DD_NUM_SYNC_TIMEOUT); DDMI_TF_SPIN in tests
   unsigned* flags = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostics (stamps build): [B][40] shader-clock stamps per phase
 };
 bool tfdec_mk_supported(int nq, int nmem, int d, int heads, int ffn, int layers);
+size_t tfdec_mk_xbuf_floats(int B);  // exchange buffer of the four-workgroup form
 bool tfdec_mk_layer_ok(const TfMkLayer& L);  // weight-image shapes of one layer (host check)
 void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st);
 

@@ -151,6 +151,19 @@ __device__ void dedup_scene(const float* pts, int* table, int* scan, int b, int*
   }
 }
 
+// Hand-off of the query groups' results to the scene's last arriving group (MI355X_MICROARCH.md hand-off table, the
+// "workgroup whose add came last" row): every published word is stored sc1 (write-through; the line leaves the
+// writer's L2) and read back with sc1 loads, and every scene's published region starts on a 128-B line no other
+// scene writes (reg_out 1920 B, the point buffers 1280 B per scene, cls through cls_x's 128-B slot), so no reader's
+// L2 can hold a partial line another group rewrote within the launch.
+__device__ inline void st_x(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline float ld_x(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // QG queries of one scene per workgroup (G = 20 / QG workgroups per scene, group gi takes queries gi QG ..): every
 // phase is per query except the mode selection and the next taps' dedup, which the scene's last arriving group runs
 template <int QG>
@@ -565,6 +578,7 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
         const float c = s + L.c6_b[0];
         SM[S_CLS + q] = c;
         a.cls_out[row0 + q] = c;
+        if constexpr (G > 1) st_x(a.cls_x + b * 32 + q0 + q, c);
       }
     }
   }
@@ -598,17 +612,28 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
     const float y = rr[1] + SM[S_PTS + 2 * t + 1];
     const float hd = tanhf(rr[2]) * 3.14159265358979323846f;
     float* ro = a.reg_out + (pt0 + t) * 3;
-    ro[0] = x;
-    ro[1] = y;
-    ro[2] = hd;
+    if constexpr (G > 1) {
+      st_x(ro, x);
+      st_x(ro + 1, y);
+      st_x(ro + 2, hd);
+    } else {
+      ro[0] = x;
+      ro[1] = y;
+      ro[2] = hd;
+    }
     SM[S_REG + 3 * t] = x;
     SM[S_REG + 3 * t + 1] = y;
     SM[S_REG + 3 * t + 2] = hd;
     SM[S_PN + 2 * t] = x;
     SM[S_PN + 2 * t + 1] = y;
     if (a.pts_next) {
-      a.pts_next[(pt0 + t) * 2] = x;
-      a.pts_next[(pt0 + t) * 2 + 1] = y;
+      if constexpr (G > 1) {
+        st_x(a.pts_next + (pt0 + t) * 2, x);
+        st_x(a.pts_next + (pt0 + t) * 2 + 1, y);
+      } else {
+        a.pts_next[(pt0 + t) * 2] = x;
+        a.pts_next[(pt0 + t) * 2 + 1] = y;
+      }
     }
   }
   __syncthreads();
@@ -637,39 +662,41 @@ __global__ __launch_bounds__(NT, 1) void decoder_mk_kernel(MkArgs a) {
   }
   if constexpr (G > 1) {
     // the scene-level tail (mode selection, the next taps' dedup) needs every group's queries: each group publishes
-    // its next points (the DDIM-updated points at a step's layer 1; pts_next holds layer 0's) and arrives at the
-    // scene's counter (every wave's stores drained and released at agent scope first); the last to arrive acquires,
-    // reads the scene's cls / reg / next points back and runs the tail, then resets the counter for the next launch
+    // its next points (the DDIM-updated points at a step's layer 1; pts_next holds layer 0's), all its published
+    // words sc1 (st_x), drains them and arrives at the scene's counter; the last to arrive (told by its add's return)
+    // reads the scene's cls / reg / next points back with sc1 loads and runs the tail, then resets the counter for
+    // the next launch. An add that returns G or more found a counter this launch did not start from zero (the tail
+    // would run twice or never): DD_NUM_SYNC_STATE.
     if (a.layer == 1 && a.ddim)
       for (int t = tid; t < QGP; t += NT) {
-        a.next_pts[(pt0 + t) * 2] = SM[S_PN + 2 * t];
-        a.next_pts[(pt0 + t) * 2 + 1] = SM[S_PN + 2 * t + 1];
+        st_x(a.next_pts + (pt0 + t) * 2, SM[S_PN + 2 * t]);
+        st_x(a.next_pts + (pt0 + t) * 2 + 1, SM[S_PN + 2 * t + 1]);
       }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ int last;
     if (tid == 0) {
       const unsigned old = __hip_atomic_fetch_add(a.scene_cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old >= (unsigned)G && a.flags) atomicOr(a.flags, DD_NUM_SYNC_STATE);
       last = old == (unsigned)(G - 1);
       if (last) __hip_atomic_store(a.scene_cnt + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const float* np = (a.layer == 1 && a.ddim) ? a.next_pts : a.pts_next;
     for (int t = tid; t < kQP; t += NT) {
       if (a.traj) {
         const float* ro = a.reg_out + ((int64_t)b * kQP + t) * 3;
-        SM[S_REG + 3 * t] = __builtin_nontemporal_load(ro);
-        SM[S_REG + 3 * t + 1] = __builtin_nontemporal_load(ro + 1);
-        SM[S_REG + 3 * t + 2] = __builtin_nontemporal_load(ro + 2);
+        SM[S_REG + 3 * t] = ld_x(ro);
+        SM[S_REG + 3 * t + 1] = ld_x(ro + 1);
+        SM[S_REG + 3 * t + 2] = ld_x(ro + 2);
       }
       if (a.next_rows && np) {
-        SM[S_PN + 2 * t] = __builtin_nontemporal_load(np + ((int64_t)b * kQP + t) * 2);
-        SM[S_PN + 2 * t + 1] = __builtin_nontemporal_load(np + ((int64_t)b * kQP + t) * 2 + 1);
+        SM[S_PN + 2 * t] = ld_x(np + ((int64_t)b * kQP + t) * 2);
+        SM[S_PN + 2 * t + 1] = ld_x(np + ((int64_t)b * kQP + t) * 2 + 1);
       }
     }
-    if (tid < kQ) SM[S_CLS + tid] = __builtin_nontemporal_load(a.cls_out + b * kQ + tid);
+    if (tid < kQ) SM[S_CLS + tid] = ld_x(a.cls_x + b * 32 + tid);
     __syncthreads();
   }
   if (a.traj && tid == 0) {
@@ -806,7 +833,8 @@ void launch_decoder_mk(const MkArgs& a, hipStream_t st) {
   if (a.B <= 0) return;
   if (!a.dim_t || !a.slots || !a.vrows || !a.akv || !a.ego || !a.film || !a.tfe || !a.pts || !a.imgx)
     throw std::runtime_error("decoder_mk: missing operand");
-  if (a.groups != 1 && (!a.scene_cnt || (a.layer == 1 && a.ddim && !a.next_pts) || (a.next_rows && a.layer == 0 && !a.pts_next)))
+  if (a.groups != 1 && (!a.scene_cnt || !a.cls_x || (a.layer == 1 && a.ddim && !a.next_pts) ||
+                        (a.next_rows && a.layer == 0 && !a.pts_next)))
     throw std::runtime_error("decoder_mk: query groups need the scene counters and the next-point buffers");
   static std::atomic<uint64_t> attr[3];
   auto go = [&](auto kern, int i, int g) {

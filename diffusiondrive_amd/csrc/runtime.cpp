@@ -269,6 +269,7 @@ class Model {
     std::vector<SegOp> ops;
     int segments = 0;
     int branched = 0;  // segments whose graph has more than one root (parallel branches): 0 by construction
+    int kernel_nodes = 0, other_nodes = 0;  // node types of the captured segments (memset / copy nodes: none)
   };
   // program cache keyed by the forward's shape signature; every entry belongs to the current buffer
   // generation (the cache is emptied when a workspace buffer is (re)allocated: graphs hold its pointers)
@@ -894,6 +895,7 @@ class Model {
         if (m.groups > 1) {
           m.scene_cnt = reinterpret_cast<unsigned*>(buf_zeroed("mk_scene_cnt", (size_t)B));
           m.next_pts = buf("mk_next_pts", (size_t)R * P * 2);
+          m.cls_x = buf("mk_cls_x", (size_t)B * 32);
         }
         if (mk_stamps) m.stamps = reinterpret_cast<unsigned long long*>(buf("mk_stamps" + sf, (size_t)B * 80));
         // algorithmic FLOPs of the launch: the 256-wide Linears (+ the anchor encoder at layer 0) and the
@@ -983,6 +985,15 @@ class Model {
     if (e == hipSuccess) e = hipGraphGetRootNodes(g, nullptr, &roots);
     if (e == hipSuccess && n > 0) {
       if (roots > 1) ++seg_prog->branched;
+      std::vector<hipGraphNode_t> nodes(n);
+      e = hipGraphGetNodes(g, nodes.data(), &n);
+      for (size_t i = 0; e == hipSuccess && i < n; ++i) {
+        hipGraphNodeType ty;
+        e = hipGraphNodeGetType(nodes[i], &ty);
+        if (e == hipSuccess) ++(ty == hipGraphNodeTypeKernel ? seg_prog->kernel_nodes : seg_prog->other_nodes);
+      }
+    }
+    if (e == hipSuccess && n > 0) {
       hipGraphExec_t ex = nullptr;
       e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
       if (e == hipSuccess) {
@@ -1788,8 +1799,10 @@ class Model {
         // forces a form; the stamps diagnostics take the one-workgroup kernel
         t.groups = (mk_stamps || tf_groups_env == 1) ? 1 : ((tf_groups_env == 4 || B * 4 <= 64) ? 4 : 1);
         if (t.groups == 4) {
-          t.xbuf = buf("tf_xbuf", (size_t)B * 9 * 4 * 32 * d);
-          t.sync_cnt = reinterpret_cast<unsigned*>(buf_zeroed("tf_sync_cnt", (size_t)2 * B));
+          t.xbuf_floats = tfdec_mk_xbuf_floats(B);
+          t.xbuf = buf("tf_xbuf", t.xbuf_floats);
+          t.sync_cnt_n = (size_t)2 * B;
+          t.sync_cnt = reinterpret_cast<unsigned*>(buf_zeroed("tf_sync_cnt", t.sync_cnt_n));
         }
         if (mk_stamps) t.stamps = reinterpret_cast<unsigned long long*>(buf("tf_stamps", (size_t)B * 80));
         // 2 x rows x sum(K x N): per layer q|k|v, 2 out_proj, cross q, FFN (+ the attention products), hoists
@@ -2535,6 +2548,20 @@ int dd_graph_info(dd_handle* h, int* programs, int* segments, int* multi_stream_
   });
 }
 
+int dd_graph_nodes(dd_handle* h, int* kernel_nodes, int* other_nodes) {
+  return guarded([&] {
+    if (!h) throw std::invalid_argument("null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    int nk = 0, no = 0;
+    for (auto& kv : h->m->programs) {
+      nk += kv.second.kernel_nodes;
+      no += kv.second.other_nodes;
+    }
+    if (kernel_nodes) *kernel_nodes = nk;
+    if (other_nodes) *other_nodes = no;
+  });
+}
+
 int dd_get_streams(dd_handle* h, int* n) {
   return guarded([&] {
     if (!h || !n) throw std::invalid_argument("null argument");
@@ -2588,6 +2615,15 @@ int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear) {
     DD_HIP_CHECK(hipEventSynchronize(m.ev_out));  // a single-stream forward may have run on the caller's stream
     DD_HIP_CHECK(hipMemcpy(flags, m.num_flags, sizeof(unsigned), hipMemcpyDeviceToHost));
     if (clear) {
+      // a megakernel's inter-workgroup wait failed or found a dirty counter: every forward has completed (the
+      // synchronisations above), so the counters are re-zeroed here, ordered before any later forward
+      if (*flags & (DD_NUM_SYNC_TIMEOUT_BIT | DD_NUM_SYNC_STATE_BIT))
+        for (const char* name : {"tf_sync_cnt", "mk_scene_cnt"}) {
+          auto it = m.bufs.find(name);
+          if (it != m.bufs.end())
+            DD_HIP_CHECK(hipMemsetAsync(it->second.first, 0, std::max<size_t>(it->second.second, 4) * sizeof(float),
+                                        m.st_own));
+        }
       DD_HIP_CHECK(hipMemsetAsync(m.num_flags, 0, sizeof(unsigned), m.st_own));
       DD_HIP_CHECK(hipStreamSynchronize(m.st_own));  // cleared before any later forward's kernels run
     }

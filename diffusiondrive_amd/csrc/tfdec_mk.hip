@@ -386,18 +386,22 @@ constexpr int tNX = 3 * tL;       // exchanges per launch, each with a buffer of
 // stores drained, workgroup barrier, lane 0: agent release + vmcnt(0), relaxed arrival add, relaxed poll until
 // the counter reaches target (monotonic within a launch: the n-th barrier waits for n * tG arrivals), agent
 // acquire + vmcnt(0); workgroup barrier; then sc1 loads. A wait that outlives any healthy schedule raises a flag
-// and goes on rather than hang the device.
-__device__ inline void scene_sync(unsigned* cnt, unsigned target, unsigned* flags) {
+// and goes on rather than hang the device. The arrival checks the count its add returned: at the n-th barrier a
+// workgroup finds between (n - 1) tG (it is the first to arrive) and n tG - 1 (the last) earlier arrivals - no
+// workgroup passes barrier n before every one has arrived at it - so anything else is a counter this launch did not
+// start from zero (a stale or clobbered counter would let the wait pass early, silently): DD_NUM_SYNC_STATE.
+__device__ inline void scene_sync(unsigned* cnt, unsigned target, unsigned* flags, unsigned spin_limit) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((old >= target || old + tG < target) && flags) atomicOr(flags, DD_NUM_SYNC_STATE);
     unsigned n = 0;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++n == (1u << 22)) {
+      if (++n >= spin_limit) {
         if (flags) atomicOr(flags, DD_NUM_SYNC_TIMEOUT);
         break;
       }
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   unsigned nsync = 0;
   auto sync = [&]() {
     ++nsync;
-    scene_sync(cnt, nsync * tG, a.flags);
+    scene_sync(cnt, nsync * tG, a.flags, a.spin_limit);
   };
   auto xbuf_next = [&]() { return (int)nsync * XBUF; };  // exchange n writes buffer n (float offset)
   const __attribute__((address_space(4))) TfMkLayer* lay = (const __attribute__((address_space(4))) TfMkLayer*)a.layers;
@@ -640,7 +644,9 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   // every workgroup of the scene is past its last wait: the last to get here resets the scene's counters
   if (tid == 0) {
     unsigned* done = a.sync_cnt + a.B + b;
-    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tG - 1) {
+    const unsigned old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old >= tG && a.flags) atomicOr(a.flags, DD_NUM_SYNC_STATE);
+    if (old == tG - 1 && !a.no_reset) {
       __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -674,12 +680,18 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   }
 }
 
+__global__ void tf_zero_counters(unsigned* c, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) __hip_atomic_store(c + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 bool tfdec_mk_layer_ok(const TfMkLayer& L) {
   return L.sa_in.nks == 16 && L.sa_out.nks == 16 && L.ca_q.nks == 16 && L.ca_out.nks == 16 && L.l1.nks == 16 &&
          L.l2.nks == 64 && L.sa_in.w && L.l2.w && L.n3b;
 }
+
+size_t tfdec_mk_xbuf_floats(int B) { return (size_t)B * tNX * XBUF; }
 
 bool tfdec_mk_supported(int nq, int nmem, int d, int heads, int ffn, int layers) {
   return nq == tQ && nmem == tM && d == tD && heads == tNH && ffn == tFF && layers == tL;
@@ -691,13 +703,40 @@ void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st) {
     throw std::runtime_error("tfdec_mk: missing operand");
   if (a.groups == tG) {
     if (!a.xbuf || !a.sync_cnt) throw std::runtime_error("tfdec_mk: groups = 4 needs xbuf / sync_cnt");
+    if (a.xbuf_floats < tfdec_mk_xbuf_floats(a.B))
+      throw std::runtime_error("tfdec_mk: xbuf holds " + std::to_string(a.xbuf_floats) + " floats, groups = 4 needs " +
+                               std::to_string(tfdec_mk_xbuf_floats(a.B)));
+    if (a.sync_cnt_n < (size_t)2 * a.B) throw std::runtime_error("tfdec_mk: sync_cnt needs 2 B counters");
     static std::atomic<uint64_t> attr4;
     // the scene counters start at zero (zeroed at allocation) and the last workgroup of a scene to finish resets
-    // them; DDMI_TF_MEMSET=1 also zeroes them ahead of every launch (a memset node in the captured graph)
+    // them. Diagnostics of the round-5 replay failure (DESIGN.md §4 tfdec_mk4, tools/gpu_r6*.sh), DDMI_TF_MEMSET:
+    // 1 a memset node zeroing the counters ahead of every launch (as round 5 first had it), 2 the same memset node
+    // on a scratch buffer the kernel never reads, 3 as 1 with the kernel's own reset off, 4 the counters zeroed by
+    // a kernel node (agent-scope atomic stores) instead of the memset node
     const char* me = getenv("DDMI_TF_MEMSET");
-    if (me && atoi(me)) DD_HIP_CHECK(hipMemsetAsync(a.sync_cnt, 0, (size_t)a.B * 2 * sizeof(unsigned), st));
+    const int mset = me ? atoi(me) : 0;
+    TfMkArgs aa = a;
+    const size_t cb = (size_t)a.B * 2 * sizeof(unsigned);
+    if (mset == 1 || mset == 3) DD_HIP_CHECK(hipMemsetAsync(a.sync_cnt, 0, cb, st));
+    if (mset == 2) {
+      static void* scratch = nullptr;
+      static size_t scratch_n = 0;
+      if (scratch_n < cb) {
+        if (scratch) DD_HIP_CHECK(hipFree(scratch));
+        DD_HIP_CHECK(hipMalloc(&scratch, cb));
+        scratch_n = cb;
+      }
+      DD_HIP_CHECK(hipMemsetAsync(scratch, 0, cb, st));
+    }
+    if (mset == 3) aa.no_reset = 1;
+    // DDMI_TF_NORESET=1: the kernel leaves its counters as they are (the next launch starts dirty); DDMI_TF_SPIN=n:
+    // every wait gives up after n polls (forced timeouts). Read per dispatch (eager forwards): tests of the
+    // DD_NUM_SYNC_* flags and of the counters' state after such launches (tests/test_sync_gpu.py)
+    if (const char* e = getenv("DDMI_TF_NORESET")) aa.no_reset = aa.no_reset || atoi(e) != 0;
+    if (const char* e = getenv("DDMI_TF_SPIN")) aa.spin_limit = (unsigned)std::max(1, atoi(e));
+    if (mset == 4) hipLaunchKernelGGL(tf_zero_counters, dim3(1), dim3(256), 0, st, a.sync_cnt, 2 * a.B);
     set_max_lds_once(attr4, reinterpret_cast<const void*>(tfdec_mk4_kernel), LDS_T);
-    hipLaunchKernelGGL(tfdec_mk4_kernel, dim3(a.B * tG), dim3(NT), LDS_T, st, a);
+    hipLaunchKernelGGL(tfdec_mk4_kernel, dim3(a.B * tG), dim3(NT), LDS_T, st, aa);
     DD_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -414,7 +414,10 @@ class DiffusionDriveModel:
         ``segments`` in all, and ``multi_stream_execs`` (segments with parallel branches: always 0)."""
         p, s, m = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.dd_graph_info(self.handle, ctypes.byref(p), ctypes.byref(s), ctypes.byref(m)), self.lib)
-        return {"programs": p.value, "segments": s.value, "multi_stream_execs": m.value}
+        k, o = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.dd_graph_nodes(self.handle, ctypes.byref(k), ctypes.byref(o)), self.lib)
+        return {"programs": p.value, "segments": s.value, "multi_stream_execs": m.value, "kernel_nodes": k.value,
+                "other_nodes": o.value}
 
     def reset_stats(self):
         _lib.check(self.lib.dd_reset_stats(self.handle), self.lib)

@@ -156,6 +156,11 @@ int dd_get_streams(dd_handle* h, int* n);
 /* The captured forwards the handle holds: programs (one per shape / mode), their single-stream graph segments in all,
  * and segments whose graph has parallel branches (more than one root node: a multi-stream exec; 0 by construction). */
 int dd_graph_info(dd_handle* h, int* programs, int* segments, int* multi_stream_execs);
+/* Node types of those captured segments: kernel nodes, and every other node (memset / memcpy / event nodes). The
+ * forward captures kernel nodes only - input staging copies run on the stream ahead of the replay, outside any graph
+ * - so other_nodes is 0 (tfdec_mk4: a memset node zeroing a megakernel's counters was not seen by the
+ * kernel's memory-side atomics in graph replays). */
+int dd_graph_nodes(dd_handle* h, int* kernel_nodes, int* other_nodes);
 /* GEMM arithmetic of every conv / linear of the path:
  *   DD_GEMM_FP32   fp32-input MFMA (v_mfma_f32_32x32x2_f32), an exact fp32 fma chain;
  *   DD_GEMM_F16X3  3-product fp16 split on f16 MFMA (conv_x3.hip): each fp32 operand becomes
@@ -185,10 +190,13 @@ int dd_set_schedule(dd_handle* h, int schedule);
 /* Numerics flags raised by kernels since the last clear (synchronises the handle's stream):
  * bit 0 (DD_NUM_F16_OVERFLOW_BIT) = an activation reached |x| >= 65504 under DD_GEMM_F16X3, so that
  * forward's result is not trustworthy (re-run it in DD_GEMM_FP32); bit 1 (DD_NUM_SYNC_TIMEOUT_BIT) = the
- * tf-decoder megakernel's inter-workgroup wait gave up (never on a healthy device; same remedy).
- * clear != 0 resets them. */
+ * tf-decoder megakernel's inter-workgroup wait gave up (never on a healthy device; same remedy); bit 2
+ * (DD_NUM_SYNC_STATE_BIT) = a megakernel's inter-workgroup counter (tf decoder groups, decoder query groups) held a
+ * value no healthy launch leaves there, so the waits it guards passed or failed wrongly (same remedy).
+ * clear != 0 resets them, and after bit 1 or 2 also re-zeroes the inter-workgroup counters. */
 #define DD_NUM_F16_OVERFLOW_BIT 1u
 #define DD_NUM_SYNC_TIMEOUT_BIT 2u
+#define DD_NUM_SYNC_STATE_BIT 4u
 int dd_numerics_flags(dd_handle* h, unsigned* flags, int clear);
 /* Copy a named internal buffer (e.g. "p3", "keyval", "cross_bev", "reg_s0l1") of the last
  * forward into dst (device pointer), at most `count` floats; *actual = buffer length. */

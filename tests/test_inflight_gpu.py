@@ -72,7 +72,9 @@ def test_default_handle_has_no_multi_stream_exec(seeded_sd):
         one = m.forward(f, noise=nz)["trajectory"].cpu()
         assert float((one - outs[2]).abs().max()) <= 1e-5
         m.forward(f, noise=nz)
-        assert m.graph_info() == {"programs": 1, "segments": 1, "multi_stream_execs": 0}
+        info = m.graph_info()
+        assert {k: info[k] for k in ("programs", "segments", "multi_stream_execs", "other_nodes")} == \
+            {"programs": 1, "segments": 1, "multi_stream_execs": 0, "other_nodes": 0}, info
     finally:
         m.close()
 

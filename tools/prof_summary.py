@@ -68,7 +68,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace_dir")
     ap.add_argument("name")
-    ap.add_argument("--forwards", type=int, default=0, help="forward passes in the trace (for per-forward numbers)")
+    ap.add_argument("--forwards", type=int, default=0,
+                    help="forward passes in the trace; by default derived from the trace itself (stem_pool launches / 2: "
+                         "every forward runs the camera and the LiDAR stem once), and a given value that disagrees "
+                         "with the trace is replaced by the trace's count")
     ap.add_argument("--pmc", nargs="*", default=[])
     ap.add_argument("--note", default="")
     ap.add_argument("--pmc-kernel", default="conv_gemm", help="kernel class whose HBM bytes per launch to derive")
@@ -90,8 +93,19 @@ def main():
         res["classes"][k] = {"launches": n, "total_ms": us / 1e3, "avg_us": us / n, "share": us / total_us}
     for k, (n, us) in sorted(inst.items(), key=lambda x: -x[1][1]):
         res["instances"][k] = {"launches": n, "total_ms": us / 1e3, "avg_us": us / n}
+    stems = cls.get("stem_pool", [0, 0.0])[0]
+    derived = stems // 2 if stems and stems % 2 == 0 else 0
+    if derived and a.forwards and a.forwards != derived:
+        print(f"[prof_summary] --forwards {a.forwards} disagrees with the trace ({stems} stem_pool launches = "
+              f"{derived} forwards): using {derived}")
+    a.forwards = derived or a.forwards
+    res["forwards"] = a.forwards
+    res["forwards_source"] = "stem_pool launches / 2" if derived else ("--forwards" if a.forwards else None)
     if a.forwards:
         res["per_forward_device_ms"] = total_us / 1e3 / a.forwards
+        for v in res["classes"].values():
+            v["launches_per_forward"] = v["launches"] / a.forwards
+            v["ms_per_forward"] = v["total_ms"] / a.forwards
     if a.pmc:
         pmc = load_pmc(a.pmc)
         res["pmc"] = {}
@@ -112,10 +126,13 @@ def main():
         json.dump(res, f, indent=1)
     lines = [f"# rocprofv3 summary: {a.name}", "", a.note, "",
              f"dispatches: {len(rows)}; total device time: {total_us / 1e3:.2f} ms"
-             + (f"; per forward: {res['per_forward_device_ms']:.2f} ms" if a.forwards else ""), "",
-             "| kernel class | launches | total ms | avg us | share |", "|---|---|---|---|---|"]
+             + (f"; forwards in the trace: {a.forwards} ({res['forwards_source']}); per forward: "
+                f"{res['per_forward_device_ms']:.2f} ms" if a.forwards else ""), "",
+             "| kernel class | launches | total ms | avg us | share | launches / forward | ms / forward |",
+             "|---|---|---|---|---|---|---|"]
     for k, v in res["classes"].items():
-        lines.append(f"| {k} | {v['launches']} | {v['total_ms']:.2f} | {v['avg_us']:.1f} | {100 * v['share']:.1f}% |")
+        pf = (f"{v['launches_per_forward']:.1f} | {v['ms_per_forward']:.3f}" if a.forwards else "- | -")
+        lines.append(f"| {k} | {v['launches']} | {v['total_ms']:.2f} | {v['avg_us']:.1f} | {100 * v['share']:.1f}% | {pf} |")
     lines += ["", "| kernel instance | launches | total ms | avg us |", "|---|---|---|---|"]
     for k, v in list(res["instances"].items())[:25]:
         lines.append(f"| `{k}` | {v['launches']} | {v['total_ms']:.2f} | {v['avg_us']:.1f} |")

@@ -17,14 +17,21 @@
 //   case 4  as 0, graph [memsetD32, C]
 //   case 5  as 0, no graph: hipMemsetAsync + C launched on side directly        (stream semantics, eager)
 //   case 6  as 0, graph [C] only                                                (control: C must see the tag)
+//   case 7  as 0, graph [memset, A]: A = 256 workgroups (all XCDs), each adds 1 to counter (wg % n) with an
+//           agent-scope atomic (memory-side), writes back its XCD's L2 (agent release fence), sleeps, adds 1 again:
+//           the adds must return 0 | 1 | 2 | 3 for the two phases (4 workgroups per counter); anything else = the
+//           memset's zeros and the atomics disagree (the tfdec_mk4 counter pattern)
+//   case 8  as 7, the counters zeroed by a kernel node with agent-scope atomic stores
 //
-//   memset_node <reps> <sleep_us> [dot-dir]
+//   memset_node <reps> <sleep_us> [dot-dir|-] [words]
+// words (1..64, default 64): counters zeroed and used by cases 7 / 8 (the product zeroes 2 B words: 64 B at B = 8).
 // Prints one line per case: replays, replays in which C saw a nonzero counter, and the first bad value.
 // With dot-dir, each case's graph is written as <dot-dir>/case<k>.dot (hipGraphDebugDotPrint) to show its edges.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <string>
 
 #define CK(x)                                                                                  \
@@ -60,6 +67,22 @@ __global__ void k_check(const unsigned* cnt, unsigned* bad, unsigned* first, uns
   }
 }
 
+// A: 4 workgroups per counter, two arrival phases separated by an agent release (buffer_wbl2) + acquire
+__global__ void k_arrive(unsigned* cnt, unsigned* bad, unsigned* first, int nw) {
+  if (threadIdx.x != 0) return;
+  unsigned* c = cnt + (blockIdx.x % nw);
+  const unsigned o1 = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < 300) __builtin_amdgcn_s_sleep(4);  // ~3 us
+  const unsigned o2 = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (o1 > 7 || o2 > 7 || o2 == 0) {
+    atomicAdd(bad, 1u);
+    atomicCAS(first, 0u, 0x10000u | (o1 << 8) | o2);
+  }
+}
+
 __global__ void k_zero(unsigned* cnt) {
   if (threadIdx.x < kN) __hip_atomic_store(cnt + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -71,7 +94,8 @@ __global__ void k_noop(unsigned* p) {
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 500;
   const int sleep_us = argc > 2 ? atoi(argv[2]) : 50;
-  const char* dot = argc > 3 ? argv[3] : nullptr;
+  const char* dot = argc > 3 && std::string(argv[3]) != "-" ? argv[3] : nullptr;
+  const int nw = argc > 4 ? std::max(1, std::min(kN, atoi(argv[4]))) : kN;
   CK(hipSetDevice(0));
   hipStream_t sm, ss;
   CK(hipStreamCreateWithFlags(&sm, hipStreamNonBlocking));
@@ -85,7 +109,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&tag, sizeof(unsigned)));
   const unsigned long long ticks = (unsigned long long)sleep_us * 100ull;  // wall_clock64: 100 MHz
   int fails = 0;
-  for (int c = 0; c <= 6; ++c) {
+  for (int c = 0; c <= 8; ++c) {
     const unsigned one = 1, zero = 0;
     CK(hipMemcpy(tag, &one, sizeof(unsigned), hipMemcpyHostToDevice));
     CK(hipMemcpy(bad, &zero, sizeof(unsigned), hipMemcpyHostToDevice));
@@ -99,16 +123,23 @@ int main(int argc, char** argv) {
       CK(hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal));
       if (c == 1) hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, gs, cnt);
       if (c == 0 || c == 1 || c == 2) CK(hipMemsetAsync(cnt, 0, kN * sizeof(unsigned), gs));
-      if (c == 3) hipLaunchKernelGGL(k_zero, dim3(1), dim3(kN), 0, gs, cnt);
+      if (c == 7) CK(hipMemsetAsync(cnt, 0, nw * sizeof(unsigned), gs));
+      if (c == 3 || c == 8) hipLaunchKernelGGL(k_zero, dim3(1), dim3(kN), 0, gs, cnt);
       if (c == 4) CK(hipMemsetD32Async((hipDeviceptr_t)cnt, 0, kN, gs));
-      hipLaunchKernelGGL(k_check, dim3(1), dim3(kN), 0, gs, cnt, bad, first, tag);
+      if (c >= 7)
+        hipLaunchKernelGGL(k_arrive, dim3(4 * nw), dim3(64), 0, gs, cnt, bad, first, nw);
+      else
+        hipLaunchKernelGGL(k_check, dim3(1), dim3(kN), 0, gs, cnt, bad, first, tag);
       CK(hipStreamEndCapture(gs, &g));
       if (dot) CK(hipGraphDebugDotPrint(g, (std::string(dot) + "/case" + std::to_string(c) + ".dot").c_str(), 0));
       CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
       CK(hipGraphDestroy(g));
     }
     for (int r = 0; r < reps; ++r) {
-      if (c == 2) {
+      if (c >= 7) {  // the counters hold the last replay's final counts (8) when the graph starts
+        CK(hipEventRecord(ev, sm));
+        CK(hipStreamWaitEvent(ss, ev, 0));
+      } else if (c == 2) {
         hipLaunchKernelGGL(k_writer, dim3(1), dim3(kN), 0, ss, cnt, ticks, tag);
       } else {
         hipLaunchKernelGGL(k_writer, dim3(1), dim3(kN), 0, sm, cnt, ticks, tag);
@@ -132,7 +163,8 @@ int main(int argc, char** argv) {
     const bool expect_bad = c == 6;
     const bool ok = expect_bad ? nb == (unsigned)reps : nb == 0;
     if (!ok) ++fails;
-    std::printf("case %d: %d replays, %u saw a nonzero counter (first value %u) -> %s\n", c, reps, nb, fv,
+    std::printf("case %d: %d replays, %u %s (first value 0x%x) -> %s\n", c, reps, nb,
+                c >= 7 ? "arrivals out of range" : "saw a nonzero counter", fv,
                 ok ? "as expected" : "ORDER VIOLATED");
     std::fflush(stdout);
     if (ex) CK(hipGraphExecDestroy(ex));
