@@ -22,6 +22,9 @@
 //           the adds must return 0 | 1 | 2 | 3 for the two phases (4 workgroups per counter); anything else = the
 //           memset's zeros and the atomics disagree (the tfdec_mk4 counter pattern)
 //   case 8  as 7, the counters zeroed by a kernel node with agent-scope atomic stores
+//   case 9  as 7 with the memset in the middle of the graph: [noop, memset, A] (in the product a K / V GEMM precedes
+//           the counters' memset in the same segment)
+//   case 10 as 9 with a kernel between the memset and A: [noop, memset, noop, A]
 //
 //   memset_node <reps> <sleep_us> [dot-dir|-] [words]
 // words (1..64, default 64): counters zeroed and used by cases 7 / 8 (the product zeroes 2 B words: 64 B at B = 8).
@@ -109,7 +112,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&tag, sizeof(unsigned)));
   const unsigned long long ticks = (unsigned long long)sleep_us * 100ull;  // wall_clock64: 100 MHz
   int fails = 0;
-  for (int c = 0; c <= 8; ++c) {
+  for (int c = 0; c <= 10; ++c) {
     const unsigned one = 1, zero = 0;
     CK(hipMemcpy(tag, &one, sizeof(unsigned), hipMemcpyHostToDevice));
     CK(hipMemcpy(bad, &zero, sizeof(unsigned), hipMemcpyHostToDevice));
@@ -121,9 +124,10 @@ int main(int argc, char** argv) {
     if (c != 5) {
       hipGraph_t g;
       CK(hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal));
-      if (c == 1) hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, gs, cnt);
+      if (c == 1 || c >= 9) hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, gs, cnt);
       if (c == 0 || c == 1 || c == 2) CK(hipMemsetAsync(cnt, 0, kN * sizeof(unsigned), gs));
-      if (c == 7) CK(hipMemsetAsync(cnt, 0, nw * sizeof(unsigned), gs));
+      if (c == 7 || c >= 9) CK(hipMemsetAsync(cnt, 0, nw * sizeof(unsigned), gs));
+      if (c == 10) hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, gs, cnt);
       if (c == 3 || c == 8) hipLaunchKernelGGL(k_zero, dim3(1), dim3(kN), 0, gs, cnt);
       if (c == 4) CK(hipMemsetD32Async((hipDeviceptr_t)cnt, 0, kN, gs));
       if (c >= 7)
