@@ -22,7 +22,7 @@ ARCH = os.environ.get("DDMI_ARCH", "gfx950")
 VARIANT = os.environ.get("DDMI_BUILD_VARIANT", "")
 LIB = os.path.join(HERE, "libddmi.so") if not VARIANT else os.path.join(HERE, "_variants", f"libddmi_{VARIANT}.so")
 VARIANT_FLAGS = {"": [], "stamps": ["-DDDMI_MK_STAMPS"], "nopv": ["-DDDMI_MK_STAMPS", "-DDDMI_MK_NOPV"], "x5st": ["-DDDMI_X5_STAMPS"], "x6st": ["-DDDMI_X6_STAMPS"], "nobar": ["-DDDMI_X5_NOBAR", "-DDDMI_X5_STAMPS"], "x6nb": ["-DDDMI_X6_NOBAR"], "vust": ["-DDDMI_VU_STAMPS"], "dbg": ["-g", "-DDDMI_SEGV_TRACE"]}[VARIANT]
-SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "basicblock.hip", "elementwise.hip", "decoder.hip", "decoder_mk.hip", "tfdec_mk.hip", "bevproj.hip", "value_proj.hip", "attention.hip", "gpt_tail.hip", "stem_pool.hip", "features.hip", "train_loss.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
+SOURCES = ["conv_gemm.hip", "conv_x3.hip", "conv_x5.hip", "conv_x6.hip", "elementwise.hip", "decoder.hip", "decoder_mk.hip", "tfdec_mk.hip", "bevproj.hip", "value_proj.hip", "attention.hip", "gpt_tail.hip", "stem_pool.hip", "features.hip", "train_loss.hip", "weights.cpp", "runtime.cpp", "ops_abi.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", CSRC, "-I", INCLUDE] + VARIANT_FLAGS
 # Elementwise / decoder arithmetic must round like PyTorch-CPU's separate mul and add kernels

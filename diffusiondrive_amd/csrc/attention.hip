@@ -526,20 +526,18 @@ void launch_gpt_attention(const float* qkv, int B, int T, int C, int heads, floa
   const int hs = C / heads;
   if (prec != 0) {
     // f16x3 form: T % 32 == 0, NW (waves per workgroup) = the largest divisor of T / 32 that is <= DDMI_ATTN_NW
-    // (DDMI_ATTN_NW128 at hs = 128)
+    // (DDMI_ATTN_NW128 at hs = 128; compile-time constants, profiles/round3_i_attn_ss.txt)
     if (T % 32 || T > 1024 || (reinterpret_cast<uintptr_t>(qkv) & 15) || C % 4)
       throw std::runtime_error("gpt_attention(f16x3): T % 32 == 0, T <= 1024, 16-B aligned qkv, C % 4 == 0");
     const int nq = T / 32;
     // the largest instantiated wave count (10, 5, 4, 3, 2, 1) <= the cap that divides T / 32
     int nw = hs >= 128 ? DDMI_ATTN_NW128 : DDMI_ATTN_NW;
-    if (const char* ne = getenv(hs >= 128 ? "DDMI_ATTN_NW128" : "DDMI_ATTN_NW")) nw = std::max(1, std::min(10, atoi(ne)));
     while (nw > 1 && (nq % nw || (nw > 5 && nw != 10))) --nw;
     const float scale = (float)(1.0 / std::sqrt((double)hs));
     const dim3 grid((unsigned)((int64_t)B * heads * (nq / nw))), block((unsigned)(64 * nw));
-    // score operand splits: DDMI_ATTN_SS (read per dispatch; A/B and precision studies) else DDMI_ATTN_SS_DEFAULT
-    const char* se = getenv("DDMI_ATTN_SS");
-    const int ss = se ? atoi(se) : (prec == 2 ? 3 : DDMI_ATTN_SS_DEFAULT);
-    if (ss != 2 && ss != 3) throw std::runtime_error("gpt_attention(f16x3): DDMI_ATTN_SS must be 2 or 3");
+    // score operand splits: three-way (six products) for prec 2 (the bf16 mode's attention), else
+    // DDMI_ATTN_SS_DEFAULT (two-way, f16x3's three products)
+    const int ss = prec == 2 ? 3 : DDMI_ATTN_SS_DEFAULT;
     const size_t lds = (size_t)(hs >= 64 ? 1 : 2) * (ss * 32 * (hs + 8) + 2 * hs * 36) * 2 + (size_t)nw * 32 * sizeof(float);
     auto go = [&](auto HSC) {
       constexpr int HS = decltype(HSC)::value;

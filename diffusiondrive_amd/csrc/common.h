@@ -66,9 +66,6 @@ struct ConvArgs {
   // partials, summed in split order by a reduce launch that applies the epilogue; null: no split
   float* split_part = nullptr;
   int64_t split_cap = 0;  // floats
-  // per-tile arrival counters (>= 64, zeroed once, self-resetting): the last split of a tile sums the partials and
-  // applies the epilogue itself (no reduce launch); null: the reduce launch
-  unsigned* split_cnt = nullptr;
   int batch = 1, zdiv = 1;
   int64_t in_z1 = 0, in_z2 = 0, w_z1 = 0, w_z2 = 0, out_z1 = 0, out_z2 = 0, res_z1 = 0, res_z2 = 0;
   int64_t flops_K = -1;  // algorithmic K per output (excluding channel padding); -1 = KH*KW*Cin
@@ -290,9 +287,6 @@ __device__ inline bool epi_quads(const ConvArgs& a, const Acc (&acc)[TM][TN], ch
 #endif
 void launch_conv_gemm(const ConvArgs& a, hipStream_t st);
 void launch_conv_x3(const ConvArgs& a, hipStream_t st);
-// Fused BasicBlock (basicblock.hip): c1 = conv1 (x -> intermediate, ReLU), c2 = conv2 (intermediate -> y, residual x,
-// ReLU, optional pool_out) of a 64-channel stride-1 block; false (nothing launched) when the shapes do not fit.
-bool launch_basicblock(const ConvArgs& c1, const ConvArgs& c2, hipStream_t st);
 // Fused stem conv 7x7/2 (Cin 4, Cout 64, f16x3) + bias + ReLU + maxpool 3x3/2 into pool_out (B,Hp,Wp,64)
 // (stem_pool.hip); false when `a` is not such a stem (then nothing is launched).
 // src (optional): the device word holding the address of the reference's NCHW input of src_c channels (read by the
@@ -329,22 +323,17 @@ struct VprojArgs {
   const int* rows = nullptr;
   const int* counts = nullptr;
   int B = 0, cap = 0;
-  float* part = nullptr;
-  unsigned* tile_cnt = nullptr;
+  float* part = nullptr;  // the union form's split partials (usplit > 1): [usplit][B * cap][256]
   float* out = nullptr;
   unsigned* flags = nullptr;
-  int max_splits = 3;  // 1..3 (DDMI_VPROJ_SPLITS: tests / A/B)
-  int max_wgs = 256;   // workgroup budget for (tiles x splits): the CUs not held by a concurrent kernel
-  int nsplit = 1;      // 1: 256-channel tiles (K split up to max_splits); 2: two 128-channel halves, no K split
-  // nsplit 2: the union-staged kernel, then the gathered one for the tiles it flagged (fb: [tiles][2] words, zero
-  // between launches); union 0 = the gathered kernel for every tile (DDMI_VPROJ_UNION=0)
+  // the union-staged kernel, then the gathered one for the tiles it flagged (fb: [tiles][2] words, zero between
+  // launches); union 0 = the gathered kernel for every tile (DDMI_VPROJ_UNION=0)
   int union_stage = 1;
   int umax = 1 << 30;  // union size above which a tile falls back (tests: DDMI_VPROJ_UMAX; the kernel's capacity rules)
   unsigned* fb = nullptr;
   int fb_only = 0;     // (set by launch_vproj) the gathered kernel computes only the flagged (tile, half) pairs
   int usplit = 1;      // union form: K split over the 16 channel groups (1, 2, 4, 8, 16); partials in `part`
   unsigned* ucnt = nullptr;  // union form with usplit > 1: [tiles][2] arrival counters, zero between launches
-  int diag = 0;              // timing diagnostic (DDMI_VPROJ_DIAG, read per dispatch): bit 0 = union loads read nothing, bit 1 = B DMAs read nothing (WRONG results)
 };
 bool vproj_supported(int C, int Cout, int H, int W);
 size_t vproj_tiles(int B, int cap);

@@ -418,75 +418,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int M
   }
 
   if constexpr (SPLIT) {
-    if (a.split_cnt) {
-      // fused hand-off (value_proj.hip's form): partials stored write-through (sc1), drained, one agent-scope add per
-      // workgroup on the tile's counter; the last adder resets it, loads the other splits' partials (sc1) and sums
-      // all S in split order - the reduce launch's order and epilogue expressions
-      __shared__ int s_last;
-      const __amdgpu_buffer_rsrc_t rp = make_rsrc(a.split_part);
-      auto poff = [&](int s2, int m, int n) { return (uint32_t)((((int64_t)s2 * M + m) * a.Cout + n) * 4); };
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + (wn * TN + j) * 32 + li;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const float v = acc[i][j][r];  // (a bit_cast of the vector-element lvalue itself reads element 0)
-            if (m < M && n < a.Cout)
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rp, poff(sp, m, n), 0, 16);
-          }
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old = __hip_atomic_fetch_add(a.split_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (unsigned)(S - 1);
-        if (old == (unsigned)(S - 1)) {
-          __hip_atomic_store(a.split_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-      }
-      __syncthreads();
-      if (!s_last) return;
-      bool bad = false;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + (wn * TN + j) * 32 + li;
-          if (n >= a.Cout) continue;
-          const float sc = a.wsinv[n] * a.alpha, bv = a.bias ? a.bias[n] : 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (m >= M) continue;
-            const float own = acc[i][j][r];
-            // all (up to 8) splits' loads issued before the ordered sum (unconditional: past S reads the OOB zero)
-            float p[8];
-#pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2)
-              p[s2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                    rp, s2 < S && s2 != sp ? poff(s2, m, n) : kOOB, 0, 16));
-            float sum = sp == 0 ? own : p[0];
-#pragma unroll
-            for (int s2 = 1; s2 < 8; ++s2)
-              if (s2 < S) sum += s2 == sp ? own : p[s2];
-            bad |= !__builtin_isfinite(sum);
-            const int ow = m % a.Wo, t2 = m / a.Wo, oh = t2 % a.Ho, im = t2 / a.Ho;
-            const float rv = a.res ? a.res[im * a.res_sn + oh * a.res_sh + ow * a.res_sw + n] : 0.f;
-            float v = sum * sc + bv + rv;
-            if (a.relu) v = fmaxf(v, 0.f);
-            a.out[im * a.out_sn + oh * a.out_sh + ow * a.out_sw + n] = v;
-          }
-        }
-      if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
-      return;
-    }
     // raw partial accumulators, C layout: lanes 0-31 of a register hold 32 consecutive channels of one row
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -592,37 +523,24 @@ static void launch_x3_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 }
 
 // the K-split partials summed in split order, then conv_x3's epilogue (scale, bias, residual, ReLU, strided NHWC out)
-// (SS = S as a template parameter: every split's load is issued before the ordered sum; SS = 0: a runtime-S loop,
-// DDMI_X3_RED_LOOP=1, same order and result)
+// (SS = S as a template parameter: every split's load is issued before the ordered sum)
 template <int SS>
-__global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M, int S_rt) {
+__global__ __launch_bounds__(256) void x3_split_reduce(ConvArgs a, int M) {
   const int QN = a.Cout / 4;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)M * QN) return;
   const int m = (int)(e / QN), nq = 4 * (int)(e - (int64_t)m * QN);
-  float4 s;
-  if constexpr (SS > 0) {
-    float4 p[SS];
+  float4 p[SS];
 #pragma unroll
-    for (int sp = 0; sp < SS; ++sp)
-      p[sp] = *reinterpret_cast<const float4*>(a.split_part + ((int64_t)sp * M + m) * a.Cout + nq);
-    s = p[0];
+  for (int sp = 0; sp < SS; ++sp)
+    p[sp] = *reinterpret_cast<const float4*>(a.split_part + ((int64_t)sp * M + m) * a.Cout + nq);
+  float4 s = p[0];
 #pragma unroll
-    for (int sp = 1; sp < SS; ++sp) {
-      s.x += p[sp].x;
-      s.y += p[sp].y;
-      s.z += p[sp].z;
-      s.w += p[sp].w;
-    }
-  } else {
-    s = *reinterpret_cast<const float4*>(a.split_part + (int64_t)m * a.Cout + nq);
-    for (int sp = 1; sp < S_rt; ++sp) {
-      const float4 p = *reinterpret_cast<const float4*>(a.split_part + ((int64_t)sp * M + m) * a.Cout + nq);
-      s.x += p.x;
-      s.y += p.y;
-      s.z += p.z;
-      s.w += p.w;
-    }
+  for (int sp = 1; sp < SS; ++sp) {
+    s.x += p[sp].x;
+    s.y += p[sp].y;
+    s.z += p[sp].z;
+    s.w += p[sp].w;
   }
   const bool bad = !(__builtin_isfinite(s.x) && __builtin_isfinite(s.y) && __builtin_isfinite(s.z) &&
                      __builtin_isfinite(s.w));
@@ -667,24 +585,17 @@ static bool launch_x3_split(const ConvArgs& a, int M, int K, hipStream_t st, int
   const int ntm = (M + 63) / 64, ntn = (a.Cout + 63) / 64;
   static const std::string name = "conv_x3<64,64,f16x3,ksplit>";
   set_last_conv_config(name.c_str());
-  const char* fe = getenv("DDMI_X3_SPLIT_FUSE");  // read per dispatch; 1: the last split reduces (no reduce launch)
-  ConvArgs b = a;
-  if (!(fe && atoi(fe))) b.split_cnt = nullptr;
-  hipLaunchKernelGGL((conv_x3_kernel<2, 2, 1, 1, 1, 0, 0, 1>), dim3(ntm * ntn, S), dim3(256), 0, st, b, M, K, ntm,
+  hipLaunchKernelGGL((conv_x3_kernel<2, 2, 1, 1, 1, 0, 0, 1>), dim3(ntm * ntn, S), dim3(256), 0, st, a, M, K, ntm,
                      ntn);
   DD_HIP_CHECK(hipGetLastError());
-  if (b.split_cnt) return true;
   const int64_t quads = (int64_t)M * (a.Cout / 4);
   const dim3 rg((unsigned)((quads + 255) / 256));
-  const char* rl = getenv("DDMI_X3_RED_LOOP");
-  if (rl && atoi(rl))
-    hipLaunchKernelGGL(x3_split_reduce<0>, rg, dim3(256), 0, st, a, M, S);
-  else if (S == 2)
-    hipLaunchKernelGGL(x3_split_reduce<2>, rg, dim3(256), 0, st, a, M, S);
+  if (S == 2)
+    hipLaunchKernelGGL(x3_split_reduce<2>, rg, dim3(256), 0, st, a, M);
   else if (S == 4)
-    hipLaunchKernelGGL(x3_split_reduce<4>, rg, dim3(256), 0, st, a, M, S);
+    hipLaunchKernelGGL(x3_split_reduce<4>, rg, dim3(256), 0, st, a, M);
   else
-    hipLaunchKernelGGL(x3_split_reduce<8>, rg, dim3(256), 0, st, a, M, S);
+    hipLaunchKernelGGL(x3_split_reduce<8>, rg, dim3(256), 0, st, a, M);
   DD_HIP_CHECK(hipGetLastError());
   return true;
 }

@@ -444,17 +444,10 @@ static void launch_x5_one(const ConvArgs& a, int M, int K, hipStream_t st) {
                        ntm, ntn);
   DD_HIP_CHECK(hipGetLastError());
 }
-// NS: stages of the 32-deep form; the deep-ring form (DDMI_X5_DEEP, read per dispatch) runs 16-deep chunks in
-// the stages that fit the same LDS budget (NS16)
-template <int WM, int WN, int TM, int TN, int NS, int NS16 = 0>
+// NS: stages of the 32-deep ring. (A 16-deep ring with twice the stages, bit-identical, measured slower on every GPT
+// shape: 123.6 -> 130.7 us per 256 x 256 launch; removed in round 6, git history.)
+template <int WM, int WN, int TM, int TN, int NS>
 static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
-  if constexpr (NS16 > 0) {
-    const char* de = getenv("DDMI_X5_DEEP");
-    if (de && atoi(de) && a.prec == 0) {
-      launch_x5_one<WM, WN, TM, TN, NS16, 0, 16>(a, M, K, st);
-      return;
-    }
-  }
   if (a.prec == 1)
     launch_x5_one<WM, WN, TM, TN, NS + 1, 1, KC>(a, M, K, st);  // the freed B image buys a stage
   else
@@ -467,26 +460,12 @@ static void launch_x5_cfg(const ConvArgs& a, int M, int K, hipStream_t st) {
 // slower than conv_x3 on the GPT shapes (tools/micro/gemm_x3_bench.py) and are not routed here.
 bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   if (a.prec != 0 && a.prec != 1) return false;
-  // micro-benchmark override (tools/micro/conv_bench, tools/gpu_x5tile.sh), read per dispatch (a forward
-  // dispatches only when it is captured or run eagerly; graph replays do not come here)
-  const char* te = getenv("DDMI_X5_TILE");
-  const int t = te ? atoi(te) : 0;
-  if (t) {
-    if (t == 1) { launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st); return true; }   // 256 x 128
-    if (t == 2) { launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st); return true; }   // 256 x 256
-    if (t == 3) { launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st); return true; }   // 256 x 64
-    if (t == 4) { launch_x5_cfg<2, 2, 2, 2, 4>(a, M, K, st); return true; }   // 128 x 128, 4 waves
-    if (t == 5) { launch_x5_cfg<2, 4, 3, 2, 2>(a, M, K, st); return true; }   // 192 x 256, 8 waves
-    if (t == 6) { launch_x5_cfg<2, 2, 3, 2, 3>(a, M, K, st); return true; }   // 192 x 128, 4 waves
-    if (t == 7) { launch_x5_cfg<2, 2, 2, 2, 2>(a, M, K, st); return true; }   // 128 x 128, 4 waves, 2 stages (2 per CU)
-    if (t == 99) return false;                                                // conv_x3 / fallback
-  }
   const int64_t m256 = (M + 255) / 256;
   const int64_t n256 = (a.Cout + 255) / 256, n128 = (a.Cout + 127) / 128;
   // 1x1 stride-1 GEMMs (the GPT M = 20480 token GEMMs): 256 x 256 tiles already pay at half a chip of
   // tiles when Cout is a multiple of 256 from 512 up (MLP-down K = 2048: 172 -> 161 us, qkv C = 256:
   // 52 -> 43 us, MLP-up C = 128: 34 -> 31 us), 256 x 128 for Cout = 256 k + 128 (qkv C = 128: 25 -> 23 us);
-  // Cout = 256 GEMMs with 80 tiles stay on conv_x3 (tools/micro/conv_bench, DDMI_X5_TILE)
+  // Cout = 256 GEMMs with 80 tiles stay on conv_x3 (tools/micro/conv_bench; the round-3 tile sweep)
   const bool gemm = a.KH * a.KW == 1 && a.stride == 1;
   // short-K GEMMs with Cout = 512 / 1024 fill more of the chip with 192 x 256 tiles (proj C = 512: 61 -> 57 us,
   // MLP-up C = 256: 72 -> 65 us, C = 128: 30 -> 27 us); K = 2048 and the qkv shapes lose with the 3 x 2 wave
@@ -499,11 +478,11 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
     if (m256 < 256) return false;
     launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st);  // 256 x 64, 4 waves
   } else if (a.Cout > 128 && m256 * n256 >= 256) {
-    launch_x5_cfg<4, 2, 2, 4, 2, 4>(a, M, K, st);  // 256 x 256, 8 waves
+    launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);  // 256 x 256, 8 waves
   } else if (a.Cout <= 128 && m256 * n128 >= 256) {
     launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);  // 256 x 128, 8 waves
   } else if (gemm && a.Cout >= 512 && a.Cout % 256 == 0 && m256 * n256 >= 128) {
-    launch_x5_cfg<4, 2, 2, 4, 2, 4>(a, M, K, st);
+    launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);
   } else if (gemm && a.Cout % 256 == 128 && m256 * n128 >= 192) {
     launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);
   } else {

@@ -150,7 +150,7 @@ extern "C" int dd_x6_stamps_read(unsigned long long* h, int n) {
 // each fragment set feeds two bf16 MFMAs, ah*bh + al*bl, instead of three f16 ones - one product per MAC).
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH, int PREC>
 __global__ __launch_bounds__(64 * WM * WN, SH >= 2 ? SH + 1 : (SH ? (WM * WN == 8 ? 4 : 2) : 1)) void conv_x6_kernel(ConvArgs a, int tiles_x, int tiles_y, int n_sp,
-                                                               int ntn, int nchunks, int diag) {
+                                                               int ntn, int nchunks) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = TH * TW;
   constexpr int TM = BM / WM / 32;
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH >= 2 ? SH + 1 : (SH ? (WM * WN == 
   const int nq = n0 + 4 * qn;
   const bool nv = nq < a.Cout;
   float* out = a.out + (int64_t)nimg * a.out_sn + nq;
-  const float* res = (a.res && !(diag & 1)) ? a.res + (int64_t)nimg * a.res_sn + nq : nullptr;
+  const float* res = a.res ? a.res + (int64_t)nimg * a.res_sn + nq : nullptr;
   const int osh = (int)a.out_sh, osw = (int)a.out_sw;
   const int rsh = (int)a.res_sh, rsw = (int)a.res_sw;
   // the residual / scale / bias loads go out before the accumulators are parked, so their latency
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(64 * WM * WN, SH >= 2 ? SH + 1 : (SH ? (WM * WN == 
       v.w = fmaxf(v.w, 0.f);
     }
     // nontemporal output stores (common.h epi_quads: +0.5 % scenes/s with all three sites)
-    if (!(diag & 2)) __builtin_nontemporal_store(v, reinterpret_cast<x6f4*>(out + ooff[k]));
+    __builtin_nontemporal_store(v, reinterpret_cast<x6f4*>(out + ooff[k]));
     if (a.pool_out) *reinterpret_cast<x6f4*>(ct + p * BN + 4 * qn) = v;  // the finished value, for the pool
   }
   if (a.pool_out) {
@@ -587,12 +587,8 @@ static void launch_x6_one(const ConvArgs& a_in, hipStream_t st) {
                                   std::to_string(BN) + "," + std::to_string(WM) + "," + std::to_string(WN) +
                                   (PREC ? ",bf16>" : ">");
   set_last_conv_config(name.c_str());
-  // timing diagnostic, read per dispatch (graph replays do not dispatch): DDMI_X6_DIAG bit 0 = skip the residual
-  // read, bit 1 = skip the output store (WRONG results; tools/gpu_x6exp.sh)
-  const char* de = getenv("DDMI_X6_DIAG");
-  const int diag = de ? atoi(de) : 0;
   hipLaunchKernelGGL((conv_x6_kernel<TH, TW, BN, WM, WN, D, NSLOT, SH, PREC>), dim3(n_sp * ntn), dim3(64 * WM * WN), 0,
-                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32), diag);
+                     st, a, tiles_x, tiles_y, n_sp, ntn, a.Cin / (PREC ? 64 : 32));
   DD_HIP_CHECK(hipGetLastError());
 }
 template <int TH, int TW, int BN, int WM, int WN, int D, int NSLOT, int SH>
@@ -641,17 +637,10 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
   // (wave tile 64 x 64) with one halo buffer, two per CU - 12 % faster on the 64-channel layers,
   // 11 % slower at Cin = 256 (tools/micro/conv_bench). bf16 keeps the 8-wave form (its 64-channel halo
   // chunk would double the 4-wave form's staging registers)
-  bool sh4 = a.prec == 0 && a.Cin <= 64;
-  bool b128 = bn128;
-  bool sh8 = false;  // BN = 128 as 8-wave workgroups on 8 x 16 tiles, one halo buffer, two per CU
-  // micro-benchmark override, read per dispatch: DDMI_X6_CFG = 1 forces the 4-wave BN = 64 form, 2 the 8-wave BN = 64 form,
-  // 3 the two-per-CU BN = 128 form, 4 the 8 x 16 three-per-CU BN = 64 form for the layer-1 convs
-  const char* ce = getenv("DDMI_X6_CFG");
-  const int cf = ce ? atoi(ce) : 0;
-  if (cf == 1 && a.prec == 0) { sh4 = true; b128 = false; }
-  if (cf == 2) { sh4 = false; b128 = false; }
-  if (cf == 3 && b128 && a.prec == 0 && !wide) sh8 = true;
-  const bool sh4_3 = sh4 && cf == 4;
+  // (measured and removed in round 6, git history: a two-per-CU BN = 128 form on 8 x 16 tiles, +-4 %, and a
+  // three-per-CU BN = 64 layer-1 form, 0.3 % slower at 3 lanes in flight)
+  const bool sh4 = a.prec == 0 && a.Cin <= 64;
+  const bool b128 = bn128;
 #define X6(TH, TW, BN, WM, WN, D, NS, SH) launch_x6_cfg<TH, TW, BN, WM, WN, D, NS, SH>(a, st)
   // small grids (batches of a few scenes): the routed form would run fewer than 128 workgroups, each through the
   // whole K loop; 8 x 8 pixel tiles x 64 channels (4 waves of 32 x 32) give 4-8x the workgroups at a quarter of the
@@ -661,7 +650,7 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
     const int64_t wgs = b128 ? n_sp * ((a.Cout + 127) / 128) : n_sp * ((a.Cout + 63) / 64);
     const char* se = getenv("DDMI_X6_SMALL");
     const int sm = se ? atoi(se) : 1;
-    if (sm == 2 || (wgs < 128 && !sh8 && sm != 0)) {
+    if (sm == 2 || (wgs < 128 && sm != 0)) {
       X6(8, 8, 64, 2, 2, 2, 3, 0);
       return true;
     }
@@ -673,18 +662,8 @@ bool launch_conv_x6(const ConvArgs& a, hipStream_t st) {
       if (sh4) X6(8, 32, 64, 4, 1, 2, 3, 1); else X6(8, 32, 64, 4, 2, 2, 3, 0);
     }
   } else {
-    if (sh8) {
-      // 8 x 16 pixels x 128 channels: 23 KB halo + 3 x 16 KB ring (71 KB), wave tile 32 x 64 under 128 VGPRs: two
-      // workgroups per CU, four waves per SIMD, one's prologue / epilogue beside the other's K loop
-      X6(8, 16, 128, 4, 2, 2, 3, 1);
-    } else if (b128) {
+    if (b128) {
       X6(16, 16, 128, 4, 2, 3, 4, 0);
-    } else if (sh4_3) {
-      // opt-in: 8 x 16 pixels x 64 channels, one halo buffer: 47 KB of LDS and 167 VGPRs, three workgroups per CU
-      // (the layer-1 convs, Cin <= 64: a third resident workgroup overlaps the short K loop's prologue / epilogue;
-      // image layer 1 0.297 -> 0.288 ms, LiDAR 0.072 -> 0.069, conv_x6 8.23 -> 8.15 ms per forward, bit-identical)
-      // - but 3 lanes in flight ran 0.3 % slower with it (5461-5464 against 5471-5487 scenes/s, same box)
-      X6(8, 16, 64, 4, 1, 2, 3, 2);
     } else {
       if (sh4) X6(16, 16, 64, 4, 1, 2, 3, 1); else X6(16, 16, 64, 4, 2, 2, 3, 0);
     }

@@ -129,7 +129,7 @@ struct TfMkArgs {
   size_t xbuf_floats = 0;
   unsigned* sync_cnt = nullptr;
   size_t sync_cnt_n = 0;
-  int no_reset = 0;  // diagnostics only (DDMI_TF_MEMSET=3, DDMI_TF_NORESET): the counters are left as they are
+  int no_reset = 0;  // tests only (DDMI_TF_NORESET): the counters are left as they are
   unsigned spin_limit = 1u << 22;  // polls before a wait gives up (DD_NUM_SYNC_TIMEOUT); DDMI_TF_SPIN in tests
   unsigned* flags = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostics (stamps build): [B][40] shader-clock stamps per phase

@@ -177,19 +177,14 @@ int dd_op_conv2d_x3(const float* in, int B, int H, int W, int Cin, const float* 
     // K-split scratch, as the forward provides it (runtime.cpp: conv): small grids may take conv_x3's split form
     const int64_t mo = (int64_t)B * a.Ho * a.Wo * Cout;
     float* part = nullptr;
-    unsigned* cnt = nullptr;
     if (prec == 0 && mo <= (1 << 20)) {
       DD_HIP_CHECK(hipMalloc(&part, (size_t)(8 * mo) * sizeof(float)));
       a.split_part = part;
       a.split_cap = 8 * mo;
-      DD_HIP_CHECK(hipMalloc(&cnt, 64 * sizeof(unsigned)));
-      DD_HIP_CHECK(hipMemsetAsync(cnt, 0, 64 * sizeof(unsigned), S(stream)));
-      a.split_cnt = cnt;
     }
     launch_conv_gemm(a, S(stream));
     const hipError_t e = hipStreamSynchronize(S(stream));  // the split images die with `ar`
     if (part) DD_HIP_CHECK(hipFree(part));
-    if (cnt) DD_HIP_CHECK(hipFree(cnt));
     DD_HIP_CHECK(e);
   });
 }

@@ -197,32 +197,12 @@ class Model {
   // candidate-stream list when a branch stream shared the launch stream's hardware queue (ROCm 7.2, DESIGN.md
   // section 4, Handle lifetime) - is never used. Batches-in-flight lanes are single-stream on their callers' streams.
   bool use_side = true;
-  // f16x3: value_proj evaluated only at the grid-sample taps (DDMI_VALUE_GATHER=0: whole map)
-  bool value_gather = true;
-  bool value_dedup = true;
-  bool value_compact = true;         // DDMI_VALUE_COMPACT=0: gathered value rows in per-scene tile runs
-  bool value_splitk = true;          // DDMI_VALUE_SPLITK=0: the gathered value_proj on conv_x3 (one launch, K whole)
-  int vproj_splits = 3;              // DDMI_VPROJ_SPLITS: most K splits of value_proj.hip (1..3)
-  bool vproj_splits_env = false;     // set explicitly: also holds for single-stream handles
-  // DDMI_VPROJ_N: 2 (default) = two 128-channel N halves per row tile, no K split (no partials; exact, equal to the
-  // unsplit sum); 1 = 256-channel tiles with the K split (one at a time 4972-5017 -> 5109 scenes/s with 2, 3 in
-  // flight unchanged: profiles/round4_d_envab_if1.txt)
-  int vproj_nsplit = 2;
-  // DDMI_VPROJ_UNION: 1 (default) = the two-half form stages each row tile's 3 x 3-neighbourhood union once per
-  // channel group (value_proj.hip vproj_union_kernel); 0 = every (row, tap) gathered per K chunk
+  bool value_splitk = true;  // DDMI_VALUE_SPLITK=0: the gathered value_proj on conv_x3 (one launch, K whole)
+  // DDMI_VPROJ_UNION: 1 (default) = value_proj stages each row tile's 3 x 3-neighbourhood union once per channel
+  // group (value_proj.hip vproj_union_kernel); 0 = every (row, tap) gathered per K chunk
   bool vproj_union = true;
   bool ln_fold = true;  // DDMI_LN_FOLD=0: every GPT LayerNorm as its own launch (gemm_ln)
   int gpt_tail_env = -1;  // DDMI_GPT_TAIL=0 / 1: force the C <= 128 GPT block tail off / on (default: B <= 16)
-  // DDMI_BB_FUSE=1: layer-1 BasicBlocks as one launch each (fused_block, basicblock.hip). Off by default: measured
-  // 2.37 ms per forward against 2.06 for the two conv_x6 launches per block (profiles/round5_c_bench.json: one
-  // workgroup per CU runs its phases back to back, 39.5 us per tile against ~16 us of MFMA work)
-  int bb_fuse = 0;  // DDMI_BB_FUSE: 1 = both trunks, 2 = the LiDAR trunk only, 3 = the camera trunk only
-  // opt-in (DDMI_S0_CHUNK_MB, e.g. 72): layer 1 (stage 0) of each trunk in chunks of scenes whose output map fits
-  // that many MB (16 camera scenes of 64 x 256 x 64 = 67 MB), each chunk through all of the stage's blocks, so a
-  // chunk's maps could stay in the memory-side cache (MALL) from one conv to the next; same per-pixel arithmetic.
-  // Measured slower (one B = 64 forward at a time 4880 against 4953 scenes/s, conv_x6 8.35 against 8.07 ms: the
-  // quarter-size grids lose more than the cache saves; profiles/round5_ab.md), so off by default
-  int s0_chunk_mb = 0;
   int vproj_umax = 1 << 30;  // DDMI_VPROJ_UMAX (tests): tiles with a larger union take the gathered fallback
   int vproj_usplit_env = 0;  // DDMI_VPROJ_USPLIT (1, 2, 4, 8): the union form's K split, else chosen from B
   bool stem_nchw = true;             // see use_nchw_stem
@@ -337,21 +317,11 @@ class Model {
     st_side = pooled_stream(device);
     st = st_own = st_main;
     DD_TRACE("create model %p st_main=%p st_side=%p", (void*)this, (void*)st_main, (void*)st_side);
-    if (const char* e = getenv("DDMI_VALUE_GATHER")) value_gather = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_VALUE_DEDUP")) value_dedup = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_VALUE_COMPACT")) value_compact = atoi(e) != 0;
     if (const char* e = getenv("DDMI_VALUE_SPLITK")) value_splitk = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_VPROJ_SPLITS")) {
-      vproj_splits = std::max(1, std::min(3, atoi(e)));
-      vproj_splits_env = true;
-    }
     if (const char* e = getenv("DDMI_STEM_NCHW")) stem_nchw = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_VPROJ_N")) vproj_nsplit = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("DDMI_VPROJ_UNION")) vproj_union = atoi(e) != 0;
     if (const char* e = getenv("DDMI_LN_FOLD")) ln_fold = atoi(e) != 0;
     if (const char* e = getenv("DDMI_GPT_TAIL")) gpt_tail_env = atoi(e) != 0;
-    if (const char* e = getenv("DDMI_BB_FUSE")) bb_fuse = std::max(0, std::min(3, atoi(e)));
-    if (const char* e = getenv("DDMI_S0_CHUNK_MB")) s0_chunk_mb = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_UMAX")) vproj_umax = std::max(0, atoi(e));
     if (const char* e = getenv("DDMI_VPROJ_USPLIT")) {
       vproj_usplit_env = atoi(e);
@@ -715,7 +685,7 @@ class Model {
   // value_proj (3x3 conv 256 -> 256 + ReLU, blocks.py:68-76,114) of layer l evaluated only at the map
   // pixels the (step, layer)'s taps read: conv_x3 over the deduplicated row list `rows`
   // counts (nullable): the scenes' live-row counts - the launch then runs the scenes' rows compacted (full
-  // 128-row tiles; DDMI_VALUE_COMPACT=0 keeps one tile run per scene). Timed under its own class "value_proj";
+  // 128-row tiles; without counts one tile run per scene). Timed under its own class "value_proj";
   // its FLOPs count every row slot (2 x slots x 256 x 2304; bench.py derives the live-row rate from the counts).
   // busy_cus: CUs a kernel on the other branch holds meanwhile (the tf-decoder megakernel: one per scene)
   void gathered_value(int l, const int* rows, const int* counts, float* vrows, const float* cross, int B, int HB,
@@ -728,14 +698,14 @@ class Model {
     a.Wo = 1;
     a.rowmap = rows;
     a.rowmap_nimg = B;
-    if (value_compact && counts) {
+    if (counts) {
       a.rowcount = counts;
       a.rowcap = MR / B;
     }
     const double fl = 2.0 * MR * (double)d * 9 * dl[l].vproj.cin_real;
     const Conv& vc = dl[l].vproj;
-    if (value_splitk && value_compact && counts && vproj_supported(vc.cin, vc.cout, HB, WB) && a.wh && a.prec == 0) {
-      // value_proj.hip: compacted rows in 256 x 256 tiles, K split up to three ways, deterministic combine
+    if (value_splitk && counts && vproj_supported(vc.cin, vc.cout, HB, WB) && a.wh && a.prec == 0) {
+      // value_proj.hip: compacted rows in 256-row tiles, two 128-channel halves each
       VprojArgs v;
       v.map = cross;
       v.wh = a.wh;
@@ -747,18 +717,12 @@ class Model {
       v.counts = counts;
       v.B = B;
       v.cap = MR / B;
-      v.part = buf("vproj_part", (size_t)3 * MR * d);
-      v.tile_cnt = reinterpret_cast<unsigned*>(buf_zeroed("vproj_cnt", vproj_tiles(B, MR / B)));
       v.out = vrows;
       v.flags = num_flags;
-      // the K split only fills an otherwise idle chip: a single-stream handle (a batches-in-flight lane, sharing the
-      // device) runs unsplit, which is less work (+0.5 % scenes/s at 3 lanes; one at a time 0.25 ms per forward slower)
-      v.max_splits = (use_side || vproj_splits_env) ? vproj_splits : 1;
-      v.max_wgs = std::max(64, num_cus() - busy_cus);
-      v.nsplit = vproj_nsplit;
+      const int max_wgs = std::max(64, num_cus() - busy_cus);
       v.union_stage = vproj_union ? 1 : 0;
       v.umax = vproj_umax;
-      if (v.nsplit == 2 && v.union_stage) {
+      if (v.union_stage) {
         const size_t t8 = (vproj_tiles(B, MR / B) + 7) / 8 * 8;
         v.fb = reinterpret_cast<unsigned*>(buf_zeroed("vproj_fb", 2 * t8));
         // K split over channel groups while the (tile, half) units leave CUs idle: ~330 live rows per scene
@@ -766,7 +730,7 @@ class Model {
         // others' partials (S x 128 KB per unit), which at 16 costs more than the K loop it saves
         const int units = 2 * (int)((B * 330 + 255) / 256);
         int us = 1;
-        while (us < 8 && units * us * 2 <= v.max_wgs) us *= 2;
+        while (us < 8 && units * us * 2 <= max_wgs) us *= 2;
         if (vproj_usplit_env > 0) us = vproj_usplit_env;
         v.usplit = us;
         if (us > 1) {
@@ -1229,9 +1193,6 @@ class Model {
     if (a.wh && a.prec == 0 && mo <= (int64_t(1) << 20)) {
       a.split_cap = 8 * mo;
       a.split_part = buf(in_side ? "x3_split_side" : "x3_split_main", (size_t)a.split_cap);
-      const char* fe = getenv("DDMI_X3_SPLIT_FUSE");  // opt-in in-kernel split reduce (measured slower: round5_ab.md)
-      if (fe && atoi(fe))
-        a.split_cnt = reinterpret_cast<unsigned*>(buf_zeroed(in_side ? "x3_split_cnt_side" : "x3_split_cnt_main", 64));
     }
     launch(a.wh ? "conv_x3" : "conv_gemm", fl, [&] { launch_conv_gemm(a, st); }, &a);
     pool_done = a.pool_out && last_conv_pooled();
@@ -1256,36 +1217,6 @@ class Model {
     conv_c(c, in4, N, H, Wd, stem, true);
     launch("pool", 0, [&] { launch_maxpool3x3s2(stem, pool, N, hs, ws, c.cout, hp, wp, st); });
   }
-  // a stride-1 BasicBlock without downsample as one launch (basicblock.hip: f16x3, 64 channels, sides % 16 == 0);
-  // false (nothing launched, no pool request consumed) when it does not apply
-  template <class RP>
-  bool fused_block(const Block& blk, const float* x, int N, int H, int Wd, float* y, RP&& request_pool) {
-    const Conv &k1 = blk.c1, &k2 = blk.c2;
-    if (k1.cin != 64 || k1.cout != 64 || k2.cout != 64 || k1.k != 3 || k2.k != 3 || k1.stride != 1 || H % 16 ||
-        Wd % 16 || gemm_mode != DD_GEMM_F16X3)
-      return false;
-    const int64_t sn = (int64_t)H * Wd * 64, sh = (int64_t)Wd * 64;
-    ConvArgs a1 = conv_args(k1, x, sn, sh, 64, N, H, Wd, nullptr, sn, sh, 64, true, nullptr, 0, 0, 0);
-    if (!a1.wh || a1.prec != 0) return false;
-    const PoolSpec saved = pool_next;
-    const int saved_p = pool_next_p;
-    request_pool();
-    ConvArgs a2 = conv_args(k2, nullptr, sn, sh, 64, N, H, Wd, y, sn, sh, 64, true, x, sn, sh, 64);
-    const double fl = 2.0 * 2.0 * N * (double)H * Wd * 64.0 * 9.0 * k1.cin_real;
-    bool ok = false;
-    // algorithmic bytes: the block input once (conv1's input and conv2's residual), the output once, both convs'
-    // split weight images
-    const double by = 2.0 * N * (double)H * Wd * 64 * 4 + 2.0 * 9 * 64 * 64 * 4;
-    launch("basicblock", fl, [&] { ok = launch_basicblock(a1, a2, st); }, nullptr, by);
-    if (!ok) {  // give the pool request back to the two-launch path
-      pool_next = saved;
-      pool_next_p = saved_p;
-      return false;
-    }
-    pool_done = a2.pool_out && last_conv_pooled();
-    return true;
-  }
-
   // contiguous NHWC conv; returns output spatial size
   void conv_c(const Conv& c, const float* in, int N, int H, int Wd, float* out, bool relu, const float* res = nullptr) {
     const int Ho = (H + 2 * c.pad - c.k) / c.stride + 1, Wo = (Wd + 2 * c.pad - c.k) / c.stride + 1;
@@ -1434,22 +1365,13 @@ class Model {
     float* tmp1 = buf(tag + "_s" + std::to_string(s) + "_t1", (size_t)B * std::max(H * Wd, Ho * Wo) * mid);
     float* tmp2 = buf(tag + "_s" + std::to_string(s) + "_t2", (size_t)B * Ho * Wo * mid);
     float* dsb = buf(tag + "_s" + std::to_string(s) + "_ds", n_out);
-    // stage 0 (stride 1: every map of the stage has the input's geometry) in chunks of scenes, each chunk through
-    // every block before the next (s0_chunk); the temporaries are reused per chunk at the same addresses
-    const int64_t img_out_bytes = (int64_t)Ho * Wo * outc * 4;
-    const int per = (int)std::max<int64_t>(1, ((int64_t)s0_chunk_mb << 20) / img_out_bytes);
-    const bool bbf = bb_fuse == 1 || (bb_fuse == 2 && tag == "lid") || (bb_fuse == 3 && tag == "img");
-    const int chunk = (s == 0 && stride == 1 && s0_chunk_mb > 0 && B > per && !bbf) ? per : B;
+    // (layer 1 in MALL-sized chunks of scenes and fused BasicBlocks were measured slower and removed in round 6)
     bool all_pooled = true;
     const float* cur = x;
     int ch = H, cw = Wd;
-    for (int b0 = 0; b0 < B; b0 += chunk) {
-      const int nb = std::min(chunk, B - b0);
-      const int64_t in_img = (int64_t)H * Wd * t.ch[s], out_img = (int64_t)Ho * Wo * outc;
-      cur = x + b0 * in_img;
-      ch = H;
-      cw = Wd;
-      float* outs[2] = {bufA + b0 * out_img, bufB + b0 * out_img};
+    {
+      const int nb = B;
+      float* outs[2] = {bufA, bufB};
       for (size_t b = 0; b < blocks.size(); ++b) {
         const Block& blk = blocks[b];
         float* y = outs[b & 1];
@@ -1464,12 +1386,9 @@ class Model {
         auto request_pool = [&]() {  // square windows that tile the output exactly
           if (!last || !pool || oh % pool->oh || ow % pool->ow || oh / pool->oh != ow / pool->ow) return;
           pool_next = *pool;
-          pool_next.out += b0 * pool->sn;  // this chunk's scenes
           pool_next_p = oh / pool->oh;
         };
-        if (!blk.bottleneck && bbf && bs == 1 && !blk.has_ds && fused_block(blk, cur, nb, ch, cw, y, request_pool)) {
-          // conv1 + conv2 + identity in one launch (basicblock.hip): the intermediate stays in LDS
-        } else if (!blk.bottleneck) {
+        if (!blk.bottleneck) {
           conv_c(blk.c1, cur, nb, ch, cw, tmp2, true);
           request_pool();
           conv_c(blk.c2, tmp2, nb, oh, ow, y, true, sc);
@@ -1928,7 +1847,7 @@ class Model {
     const int R = B * Q;  // trajectory query rows
     // In f16x3 mode the conv is instead evaluated per (step, layer) at the B x Q x P x 4 bilinear taps
     // grid_sample reads (gathered rows, below): 40960 rows per call at B = 64 instead of 262144 per layer.
-    const bool gathered = value_gather && gemm_mode == DD_GEMM_F16X3 && dl[0].vproj.x3.hi != kNone &&
+    const bool gathered = gemm_mode == DD_GEMM_F16X3 && dl[0].vproj.x3.hi != kNone &&
                           dl[1].vproj.x3.hi != kNone;
     float* vals[2] = {nullptr, nullptr};
     for (int l = 0; l < 2 && !gathered; ++l) {
@@ -2027,7 +1946,7 @@ class Model {
         const std::string sfx = "_s" + std::to_string(si) + "l" + std::to_string(l);
         const int MR = R * P * 4;
         int* rows = reinterpret_cast<int*>(buf("value_taps" + sfx, (size_t)MR));
-        int* slots = value_dedup ? reinterpret_cast<int*>(buf("value_slots" + sfx, (size_t)MR)) : nullptr;
+        int* slots = reinterpret_cast<int*>(buf("value_slots" + sfx, (size_t)MR));
         float* vrows = buf("value_rows" + sfx, (size_t)MR * d);
         bool dd = false;
         if (slots)

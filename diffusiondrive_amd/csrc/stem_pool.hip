@@ -106,7 +106,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
                                                        const float* __restrict__ wsinv,
                                                        const float* __restrict__ bias, float alpha,
                                                        float* __restrict__ out, unsigned* flags, int tiles_x,
-                                                       int tiles_y, int ntiles, int diag) {
+                                                       int tiles_y, int ntiles) {
   static_assert(!ONE || SRC_C == 1, "the one-channel form reads a one-channel NCHW input");
   constexpr bool C1 = ONE;
   constexpr int KSN = C1 ? KS1 : KS;
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     tile_origin(t, b, py0, px0);
     const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;
     // ---- stem GEMM: wave (nt, mg) takes M tiles mg, mg + 4, mg + 8
-    for (int m = mg; m < NMT && !(diag & 1); m += MSTEP) {
+    for (int m = mg; m < NMT; m += MSTEP) {
       const int p = min(m * 32 + li, NSP - 1);
       const int ly = p / SW, lx = p - (p / SW) * SW;
       const int base = (2 * ly) * IP + 2 * lx + 2 * hl;  // input pixel of (kh 0, kw 2h)
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
     }
     __syncthreads();
     // ---- 3 x 3 / 2 max pool over the stem tile: (pooled pixel, channel quad) items
-    for (int i = tid; i < PH * PW * 16 && !(diag & 2); i += NT) {
+    for (int i = tid; i < PH * PW * 16; i += NT) {
       const int q = i & 15, pp = i >> 4;
       const int py = pp / PW, px = pp - (pp / PW) * PW;
       const int gy = py0 + py, gx = px0 + px;
@@ -362,10 +362,6 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   DD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int per_cu = NT == 512 ? 1 : 2;
   const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
-  // timing diagnostic, read per dispatch (graph replays do not dispatch): DDMI_STEM_DIAG bit 0 = skip the stem GEMM and
-  // its epilogue, bit 1 = skip the pool (WRONG results; tools/micro/stem_time.py)
-  const char* de = getenv("DDMI_STEM_DIAG");
-  const int diag = de ? atoi(de) : 0;
   const int c = src ? src_c : 0;
   const char* oe = getenv("DDMI_STEM1");
   const bool one = c == 1 && oe && atoi(oe) != 0;
@@ -374,7 +370,7 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
     const int lds = (c == 1 && one) ? LDS1_BYTES : LDS_BYTES;
     set_max_lds_once(attr[a.prec][c == 1 && one ? 4 : c], reinterpret_cast<const void*>(kern), lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, a.in, src, a.H, a.W, Hs, Ws, Hp, Wp, a.wh, a.wl,
-                       (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles, diag);
+                       (int)a.ldh, a.wsinv, a.bias, a.alpha, pool_out, a.flags, tiles_x, tiles_y, ntiles);
   };
   auto pick = [&](auto PR) {
     constexpr int P = decltype(PR)::value;

@@ -680,10 +680,6 @@ __global__ __launch_bounds__(NT, 1) void tfdec_mk4_kernel(TfMkArgs a) {
   }
 }
 
-__global__ void tf_zero_counters(unsigned* c, int n) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) __hip_atomic_store(c + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 }  // namespace
 
 bool tfdec_mk_layer_ok(const TfMkLayer& L) {
@@ -709,32 +705,13 @@ void launch_tfdec_mk(const TfMkArgs& a, hipStream_t st) {
     if (a.sync_cnt_n < (size_t)2 * a.B) throw std::runtime_error("tfdec_mk: sync_cnt needs 2 B counters");
     static std::atomic<uint64_t> attr4;
     // the scene counters start at zero (zeroed at allocation) and the last workgroup of a scene to finish resets
-    // them. Diagnostics of the round-5 replay failure (DESIGN.md §4 tfdec_mk4, tools/gpu_r6*.sh), DDMI_TF_MEMSET:
-    // 1 a memset node zeroing the counters ahead of every launch (as round 5 first had it), 2 the same memset node
-    // on a scratch buffer the kernel never reads, 3 as 1 with the kernel's own reset off, 4 the counters zeroed by
-    // a kernel node (agent-scope atomic stores) instead of the memset node
-    const char* me = getenv("DDMI_TF_MEMSET");
-    const int mset = me ? atoi(me) : 0;
+    // them: only agent-scope atomics ever write them. (A memset node zeroing them ahead of the kernel was not seen by
+    // the kernel's memory-side atomic arrivals in graph replays: profiles/round6_memset_node.md.)
     TfMkArgs aa = a;
-    const size_t cb = (size_t)a.B * 2 * sizeof(unsigned);
-    if (mset == 1 || mset == 3) DD_HIP_CHECK(hipMemsetAsync(a.sync_cnt, 0, cb, st));
-    if (mset == 2) {
-      static void* scratch = nullptr;
-      static size_t scratch_n = 0;
-      if (scratch_n < cb) {
-        if (scratch) DD_HIP_CHECK(hipFree(scratch));
-        DD_HIP_CHECK(hipMalloc(&scratch, cb));
-        scratch_n = cb;
-      }
-      DD_HIP_CHECK(hipMemsetAsync(scratch, 0, cb, st));
-    }
-    if (mset == 3) aa.no_reset = 1;
-    // DDMI_TF_NORESET=1: the kernel leaves its counters as they are (the next launch starts dirty); DDMI_TF_SPIN=n:
-    // every wait gives up after n polls (forced timeouts). Read per dispatch (eager forwards): tests of the
-    // DD_NUM_SYNC_* flags and of the counters' state after such launches (tests/test_sync_gpu.py)
-    if (const char* e = getenv("DDMI_TF_NORESET")) aa.no_reset = aa.no_reset || atoi(e) != 0;
+    // tests/test_sync_gpu.py, read per dispatch (eager forwards): DDMI_TF_NORESET=1 leaves the counters as they are
+    // (the next launch starts dirty), DDMI_TF_SPIN=n gives every wait up after n polls (forced timeouts)
+    if (const char* e = getenv("DDMI_TF_NORESET")) aa.no_reset = atoi(e) != 0;
     if (const char* e = getenv("DDMI_TF_SPIN")) aa.spin_limit = (unsigned)std::max(1, atoi(e));
-    if (mset == 4) hipLaunchKernelGGL(tf_zero_counters, dim3(1), dim3(256), 0, st, a.sync_cnt, 2 * a.B);
     set_max_lds_once(attr4, reinterpret_cast<const void*>(tfdec_mk4_kernel), LDS_T);
     hipLaunchKernelGGL(tfdec_mk4_kernel, dim3(a.B * tG), dim3(NT), LDS_T, st, aa);
     DD_HIP_CHECK(hipGetLastError());

@@ -1,32 +1,21 @@
 // The decoder's cross-BEV attention contraction - value_proj, a 3x3 conv 256 -> 256 + ReLU over the 64 x 64
 // cross-BEV map (modules/blocks.py:68-76,114) - evaluated only at the map pixels the grid-sample taps read
 // (blocks.py:101-122): the scenes' distinct tap pixels, counted and listed by the decoder megakernel's dedup,
-// compacted into full 256-row tiles, K split over up to three workgroups so the launch is one wave of the chip.
+// compacted into full 256-row tiles.
 //
-// Why this shape: a (step, layer) has ~21 K live rows at B = 64 (M 21 K, N 256, K 2304). conv_x3's 128 x 128 tiles
-// (332 of them: 1.3 waves) stream 32 KB of operands per 32-deep K chunk for 3 MFLOP - about the ~30 B/clk a CU
-// takes in from L2 at the MFMA rate (PMC MFMA busy 0.27). A 256 x 256 tile halves the bytes per FLOP (A 32 KB + B
-// 32 KB per chunk for 4x the work: ~15 B/clk) but there are only ~83 of them; split three ways over K they are
-// ~249 workgroups - one wave. (An earlier 128 x 256 form with the same split ran 498 workgroups, 1.95 waves, and
-// was 20 % slower than conv_x3: profiles/round3_f_vproj_splitk_ab.txt.)
+// Two kernels. The union-staged form (vproj_union_kernel, below: the default) stages each tile's union of 3 x 3
+// neighbourhoods in LDS once per channel group. The gathered form here (vproj_kernel<2>) computes the tiles whose
+// union does not fit (fb_only, right after the union launch) and every tile under DDMI_VPROJ_UNION=0.
 //
-// Splits: S = the largest of 3, 2, 1 with (live tiles) x S <= the CU budget (256, or 192 while the tf-decoder
-// megakernel holds 64 CUs beside the first launch), decided in the kernel from the live-row count (known only on the
-// device); split s of S takes K chunks [72 s / S, 72 (s + 1) / S) of the 72 (9 taps x 8 channel chunks of 32).
-//
-// Per workgroup: 8 waves (4 x 2, wave tile 64 x 128), A = the tile's gathered rows by LDS-DMA (per-lane 16-B
-// buffer loads at each row's own pixel offset; out-of-map taps read zero through the out-of-range offset), B = the
-// pre-split fp16 hi / lo weight images, 2 LDS stages (one chunk in flight under the current one's MFMAs: a chunk
-// is ~2 us of MFMAs), f16x3 products (conv_x3.hip's arithmetic), A split at fragment-read time.
-// Epilogue from the accumulators (no LDS park): C layout of 32x32 MFMA - lanes 0-31 of a register hold 32
-// consecutive channels of one row, so every store / load below is a 128-B row segment per half-wave.
-//  * S = 1: bias, ReLU, the value row out.
-//  * S > 1: every split stores its scaled partial write-through (sc1), drains, and adds to the tile's counter
-//    (agent scope); the workgroup whose add returns S - 1 - the last - loads the others' partials (sc1), sums
-//    p0 + p1 [+ p2] in that fixed order (its own from registers: deterministic whichever split arrives last), adds
-//    the bias, applies ReLU, writes the value rows where the megakernel's slots point (row b * cap + l of scene b's
-//    l-th pixel) and zeroes the counter for the next launch (MI355X_MICROARCH.md, inter-workgroup visibility:
-//    sc1 stores, one agent add per storing workgroup, the last adder told by the returned value, sc1 loads).
+// Gathered form, per workgroup: 8 waves (4 x 2, wave tile 64 x 64), a row tile's 128-channel half (the two halves
+// are two workgroups on one XCD); A = the tile's gathered rows by LDS-DMA (per-lane 16-B buffer loads at each row's
+// own pixel offset; out-of-map taps read zero through the out-of-range offset), B = the pre-split fp16 hi / lo
+// weight images, 2-3 LDS stages (chunks in flight under the current one's MFMAs), f16x3 products (conv_x3.hip's
+// arithmetic), A split at fragment-read time. Epilogue from the accumulators (no LDS park): C layout of 32x32
+// MFMA - lanes 0-31 of a register hold 32 consecutive channels of one row, so every store below is a 128-B row
+// segment per half-wave: bias, ReLU, the value row out where the megakernel's slots point (row b * cap + l of scene
+// b's l-th pixel). (A 256-channel form with the K split over three workgroups and a partial combine measured slower
+// than the halves - profiles/round3_f_vproj_splitk_ab.txt, round4 - and was removed in round 6, git history.)
 #include "common.h"
 
 namespace ddmi {
@@ -50,8 +39,7 @@ constexpr int VP_AB = VP_BM * VP_KC * 4;   // A stage bytes: fp32 rows of 128 B
 constexpr int VP_A_IN = VP_BM / 8 / VP_NW;   // A DMA instructions per wave per chunk
 static_assert(VP_A_IN >= 1, "DMA split over the waves");
 static_assert(VP_BM == 256, "the compacted row table holds 256 rows");
-// Tile width: TN = 4 -> 256 output channels (every one; the K split fills the chip), TN = 2 -> 128 (the two N halves
-// of a row tile are two workgroups on one XCD, no K split and no partials)
+// Tile width: TN = 2 -> 128 output channels (the two N halves of a row tile are two workgroups on one XCD)
 template <int TN>
 struct VpTile {
   static constexpr int BN = VP_WN * TN * 32;
@@ -105,13 +93,6 @@ __device__ inline void vp_split8(const float4& p, const float4& q, vp_h8& hi, vp
 // cache-policy bits of the raw buffer intrinsics: sc1 (write-through stores, L1-bypassing loads)
 constexpr int kSC1 = 16;
 
-// splits for a launch with `tiles` live 256-row tiles: the most (<= 3) that keep the grid within one wave of the
-// `budget` CUs this launch has (the whole chip, or what a concurrent kernel leaves: one workgroup per CU here)
-__device__ inline int vp_splits(int tiles, int cap, int budget) {
-  const int s = tiles * 3 <= budget ? 3 : (tiles * 2 <= budget ? 2 : 1);
-  return s < cap ? s : cap;
-}
-
 }  // namespace
 
 template <int VP_TN>
@@ -119,43 +100,34 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
   constexpr int VP_BN = VpTile<VP_TN>::BN, VP_BB = VpTile<VP_TN>::BB, VP_STAGE = VpTile<VP_TN>::STAGE;
   constexpr int VP_B_IN = VpTile<VP_TN>::B_IN;
   constexpr int NH = kC / VP_BN;  // N parts of a row tile
+  static_assert(NH == 2, "the two 128-channel halves of a row tile");
   constexpr int NST = VpTile<VP_TN>::NSTAGE;
   __shared__ __attribute__((aligned(1024))) char lds[NST * VP_STAGE];
   __shared__ int g_rows[VP_BM];
   __shared__ int g_pre[257];
-  __shared__ int g_last;
   const uint32_t lds_u32 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
-  if constexpr (NH > 1) {
-    // after the union-staged kernel: only the (tile, half) pairs it handed over (their flags cleared here)
-    if (a.fb_only) {
-      const int bq = blockIdx.x / (8 * NH), rq = blockIdx.x % (8 * NH);
-      const int f = (bq * 8 + rq % 8) * NH + rq / 8;
-      if (__hip_atomic_load(a.fb + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-      __syncthreads();  // every thread read the flag before it is cleared
-      if (threadIdx.x == 0) a.fb[f] = 0u;
-    }
+  // after the union-staged kernel: only the (tile, half) pairs it handed over (their flags cleared here)
+  if (a.fb_only) {
+    const int bq = blockIdx.x / (8 * NH), rq = blockIdx.x % (8 * NH);
+    const int f = (bq * 8 + rq % 8) * NH + rq / 8;
+    if (__hip_atomic_load(a.fb + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    __syncthreads();  // every thread read the flag before it is cleared
+    if (threadIdx.x == 0) a.fb[f] = 0u;
   }
   // ---- compacted rows: launch row m = the m-th live row over the scenes in order
   rowcount_prefix(a.counts, a.B, g_pre);
   const int total = g_pre[a.B];
   const int tiles = (total + VP_BM - 1) / VP_BM;
-  const int S = NH > 1 ? 1 : vp_splits(tiles, a.max_splits, a.max_wgs);
-  int bid = blockIdx.x;
-  int nh = 0;
-  if constexpr (NH > 1) {
-    // the NH halves of row tile m take blocks with equal blockIdx % 8 (one XCD under round-robin placement: the
-    // second half finds the gathered A rows in that XCD's L2; speed only)
-    const int g = bid / (8 * NH), r = bid % (8 * NH);
-    nh = r / 8;
-    bid = g * 8 + r % 8;
-  }
-  if (bid >= tiles * S) return;  // workgroup-uniform; touches no counter
-  const int mt = bid / S, sp = bid - mt * S;
+  // the NH halves of row tile m take blocks with equal blockIdx % 8 (one XCD under round-robin placement: the
+  // second half finds the gathered A rows in that XCD's L2; speed only)
+  const int nh = (blockIdx.x % (8 * NH)) / 8;
+  const int mt = blockIdx.x / (8 * NH) * 8 + blockIdx.x % 8;
+  if (mt >= tiles) return;  // workgroup-uniform
   const int m0 = mt * VP_BM;
   const int n0 = nh * VP_BN;
-  const int kbeg = sp * VP_NK / S, kend = (sp + 1) * VP_NK / S;
+  constexpr int kbeg = 0, kend = VP_NK;
   for (int r = tid; r < VP_BM; r += VP_NT) {
     const int g = m0 + r;
     int idx = -1;
@@ -314,7 +286,7 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         bad |= !__builtin_isfinite(acc[i][j][r]);
-        acc[i][j][r] *= sc[j];  // the scaled partial
+        acc[i][j][r] *= sc[j];
       }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
   auto row_of = [&](int i, int r) { return (wm * VP_TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh; };
@@ -322,72 +294,12 @@ __global__ __launch_bounds__(VP_NT) void vproj_kernel(VprojArgs a) {
     const int ri = g_rows[row_of(i, r)];
     if (ri >= 0) a.out[(int64_t)ri * kC + n0 + (wn * VP_TN + j) * 32 + li] = fmaxf(v + bias[j], 0.f);
   };
-  if (NH > 1 || S == 1) {
-#pragma unroll
-    for (int i = 0; i < VP_TM; ++i)
-#pragma unroll
-      for (int j = 0; j < VP_TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) finish(i, j, r, acc[i][j][r]);
-    return;
-  }
-  if constexpr (NH > 1) return;
-  // ---- this split's partial out, write-through; every storing wave drains before the counter add
-  const int64_t MR = (int64_t)a.B * a.cap;
-  const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, (int)kOOBv, 0x00020000);
-  auto part_off = [&](int s, int i, int j, int r) {
-    return (int)((((int64_t)s * MR + m0 + row_of(i, r)) * VP_BN + (wn * VP_TN + j) * 32 + li) * 4);
-  };
 #pragma unroll
   for (int i = 0; i < VP_TM; ++i)
 #pragma unroll
     for (int j = 0; j < VP_TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (m0 + row_of(i, r) < total) {
-          const float v = acc[i][j][r];  // (a bit_cast of the vector-element lvalue itself reads element 0)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rpart, part_off(sp, i, j, r), 0, kSC1);
-        }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    // the sc1 / drained / one-adder / sc1-load form above is the measured hand-off of MI355X_MICROARCH.md's table
-    // (row 1); the agent-scope release before the add and the acquire after it make the ordering the memory
-    // model's, not the cache-policy bits' (one each per workgroup; the compiler-hazard wait after the release)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(a.tile_cnt + mt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    g_last = old == (unsigned)(S - 1);
-    if (old == (unsigned)(S - 1)) {
-      __hip_atomic_store(a.tile_cnt + mt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!g_last) return;
-  // ---- the last split: p0 + p1 [+ p2] in split order (its own from registers, the others by sc1 loads)
-#pragma unroll
-  for (int i = 0; i < VP_TM; ++i)
-#pragma unroll
-    for (int j = 0; j < VP_TN; ++j) {
-      float p[3][16];
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        if (s >= S) break;
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          p[s][r] = (s == sp || m0 + row_of(i, r) >= total)
-                        ? acc[i][j][r]
-                        : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rpart, part_off(s, i, j, r), 0, kSC1));
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = p[0][r] + p[1][r];
-        if (S == 3) v = v + p[2][r];
-        finish(i, j, r, v);
-      }
-    }
+      for (int r = 0; r < 16; ++r) finish(i, j, r, acc[i][j][r]);
 }
 
 // ==================================================================================================================
@@ -621,7 +533,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
 #pragma unroll
     for (int i = 0; i < VU_ALD; ++i) {
       const int e = tid + VU_NT * i, u = e >> 2;
-      const bool ok = gv && u < U && !(a.diag & 1);
+      const bool ok = gv && u < U;
       const int o = ok ? g_upix[u] * kC + 4 * (e & 3) + g * 16 : 0;
       hr[i] = vu_vload(rin, ok ? (uint32_t)o * 4u : kOOBv);
     }
@@ -661,7 +573,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
   const bool bimg_lo = (wave * VU_BPS) / VU_BQ == 1;
   const vp_i4 rwb = vp_rsrc(bimg_lo ? (const void*)a.wl : (const void*)a.wh);
   auto b_issue = [&](int slot, int tap, int g) {
-    const bool gv = g < gend && !(a.diag & 2);
+    const bool gv = g < gend;
     const uint32_t kb = (uint32_t)(tap * kC + g * 16) * 2u;
 #pragma unroll
     for (int j = 0; j < VU_BPS; ++j) {
@@ -863,7 +775,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         bad |= g_rows[row_of(i, r)] >= 0 && !__builtin_isfinite(acc[i][j][r]);
-        acc[i][j][r] *= sc[j];  // the scaled partial
+        acc[i][j][r] *= sc[j];
       }
   if (bad && a.flags) atomicOr(a.flags, (unsigned)DD_NUM_F16_OVERFLOW);
   auto finish = [&](int i, int j, int r, float v) {
@@ -905,6 +817,8 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned* cnt = a.ucnt + mt * 2 + nh;
     const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a count at or past S: this launch did not start the counter from zero (the sum would run twice or never)
+    if (old >= (unsigned)S && a.flags) atomicOr(a.flags, DD_NUM_SYNC_STATE);
     g_usize = old == (unsigned)(S - 1);
     if (old == (unsigned)(S - 1)) {
       __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -955,44 +869,33 @@ bool vproj_supported(int C, int Cout, int H, int W) { return C == kC && Cout == 
 size_t vproj_tiles(int B, int cap) { return ((size_t)B * cap + VP_BM - 1) / VP_BM; }
 
 void launch_vproj(const VprojArgs& a, hipStream_t st) {
-  if (!a.map || !a.wh || !a.wl || !a.wsinv || !a.bias || !a.rows || !a.counts || !a.part || !a.tile_cnt || !a.out)
+  if (!a.map || !a.wh || !a.wl || !a.wsinv || !a.bias || !a.rows || !a.counts || !a.out)
     throw std::runtime_error("vproj: missing operand");
-  if (a.B < 1 || a.B > 256 || a.cap < 1 || a.ldh < 9 * kC || a.ldh % 8 || a.max_splits < 1 || a.max_splits > 3 ||
-      a.max_wgs < 1)
-    throw std::runtime_error("vproj: B in [1, 256], ldh >= 2304 and a multiple of 8, max_splits in [1, 3]");
+  if (a.B < 1 || a.B > 256 || a.cap < 1 || a.ldh < 9 * kC || a.ldh % 8)
+    throw std::runtime_error("vproj: B in [1, 256], ldh >= 2304 and a multiple of 8");
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  if (!al16(a.map) || !al16(a.wh) || !al16(a.wl) || !al16(a.wsinv) || !al16(a.bias) || !al16(a.part) || !al16(a.out))
+  if (!al16(a.map) || !al16(a.wh) || !al16(a.wl) || !al16(a.wsinv) || !al16(a.bias) || !al16(a.out) ||
+      (a.part && !al16(a.part)))
     throw std::runtime_error("vproj: operands must be 16-byte aligned");
-  // buffer offsets are 32-bit byte offsets below 2^31
-  if ((int64_t)a.B * kHW * kHW * kC * 4 >= (int64_t)kOOBv || (int64_t)3 * a.B * a.cap * kC * 4 >= (int64_t)kOOBv ||
-      (int64_t)kC * a.ldh * 2 >= (int64_t)kOOBv)
+  // buffer offsets are 32-bit byte offsets below 2^31: the map, the weight images and the union split's partials
+  // (usplit slabs of B * cap rows)
+  if ((int64_t)a.B * kHW * kHW * kC * 4 >= (int64_t)kOOBv || (int64_t)kC * a.ldh * 2 >= (int64_t)kOOBv ||
+      (a.union_stage && (int64_t)a.usplit * a.B * a.cap * kC * 4 >= (int64_t)kOOBv))
     throw std::runtime_error("vproj: operand extent >= 2 GiB");
-  if (a.nsplit == 2) {
-    // two 128-channel halves per row tile, no K split: grid in groups of 8 tiles x 2 halves
-    const size_t t8 = (vproj_tiles(a.B, a.cap) + 7) / 8 * 8;
-    if (a.union_stage) {
-      if (!a.fb || (a.usplit > 1 && (!a.ucnt || !a.part)) || (a.usplit & (a.usplit - 1)) || a.usplit > 8)
-        throw std::runtime_error("vproj: the union-staged form needs fallback flags, a power-of-two split <= 8 "
-                                 "and, split, its counters and partials");
-      VprojArgs u = a;
-      if (const char* de = getenv("DDMI_VPROJ_DIAG")) u.diag = atoi(de);
-      // DDMI_VPROJ_BAR=1: a step barrier at every step (A/B of the BAR2 schedule; same arithmetic)
-      const char* be = getenv("DDMI_VPROJ_BAR");
-      if (be && atoi(be) == 1)
-        hipLaunchKernelGGL(vproj_union_kernel<false>, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, u);
-      else
-        hipLaunchKernelGGL(vproj_union_kernel<true>, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, u);
-      DD_HIP_CHECK(hipGetLastError());
-      VprojArgs f = a;
-      f.fb_only = 1;  // tiles whose union did not fit: the gathered form
-      hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, f);
-    } else {
-      hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, a);
-    }
+  // two 128-channel halves per row tile: grid in groups of 8 tiles x 2 halves
+  const size_t t8 = (vproj_tiles(a.B, a.cap) + 7) / 8 * 8;
+  if (a.union_stage) {
+    if (!a.fb || (a.usplit > 1 && (!a.ucnt || !a.part)) || a.usplit < 1 || (a.usplit & (a.usplit - 1)) ||
+        a.usplit > 8)
+      throw std::runtime_error("vproj: the union-staged form needs fallback flags, a power-of-two split <= 8 "
+                               "and, split, its counters and partials");
+    hipLaunchKernelGGL(vproj_union_kernel<true>, dim3((unsigned)(t8 * 2 * a.usplit)), dim3(VU_NT), 0, st, a);
+    DD_HIP_CHECK(hipGetLastError());
+    VprojArgs f = a;
+    f.fb_only = 1;  // tiles whose union did not fit: the gathered form
+    hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, f);
   } else {
-    // every (tile, split) the kernel may pick: up to 3 splits of every possible tile
-    const dim3 grid((unsigned)(vproj_tiles(a.B, a.cap) * 3));
-    hipLaunchKernelGGL(vproj_kernel<4>, grid, dim3(VP_NT), 0, st, a);
+    hipLaunchKernelGGL(vproj_kernel<2>, dim3((unsigned)(t8 * 2)), dim3(VP_NT), 0, st, a);
   }
   DD_HIP_CHECK(hipGetLastError());
 }

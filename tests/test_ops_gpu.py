@@ -165,38 +165,6 @@ def test_conv2d_f16x3_b64_routes(gpu, B, H, W, Cin, Cout, k, s, p, relu, res, ro
     assert int(flags.item()) == 0
 
 
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [
-    (8, 64, 256, 64, 64),    # image layer 1 shape (8 scenes)
-    (16, 64, 64, 64, 64),    # LiDAR layer 1 shape
-    (32, 36, 52, 32, 64),    # ragged tiles, Cin = 32 (one chunk)
-])
-def test_conv2d_three_per_cu_form_is_bit_identical(gpu, monkeypatch, B, H, W, Cin, Cout):
-    """The opt-in layer-1 form (DDMI_X6_CFG=4): 4 waves, BN = 64 on 8 x 16 tiles with one halo buffer, three
-    workgroups per CU, against the routed 16 x 16 two-per-CU form: the same K order, so bit-identical outputs."""
-    x = rnd(B, Cin, H, W, seed=81)
-    w = rnd(Cout, Cin, 3, 3, seed=82, scale=1.0 / np.sqrt(Cin * 9))
-    b = rnd(Cout, seed=83)
-    r = rnd(B, Cout, H, W, seed=84)
-    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
-
-    def run(cfg):
-        if cfg:
-            monkeypatch.setenv("DDMI_X6_CFG", cfg)
-        else:
-            monkeypatch.delenv("DDMI_X6_CFG", raising=False)
-        out = torch.empty(B, H, W, Cout, device=DEV)
-        flags = torch.zeros(1, dtype=torch.int32, device=DEV)
-        ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
-                               out.data_ptr(), Cout, 3, 3, 1, 1, 1, 0, flags.data_ptr(), None), gpu)
-        assert int(flags.item()) == 0
-        return out, gpu.dd_op_last_kernel().decode()
-
-    three, route = run("4")
-    routed, route0 = run("")
-    assert route == "conv_x6<8,16,64,4,1>" and route0 == "conv_x6<16,16,64,4,1>", (route, route0)
-    assert torch.equal(three, routed)
-
-
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [
     (1, 8, 32, 512, 512),    # image layer 4 at batch 1
@@ -273,80 +241,9 @@ def test_conv_x3_k_split(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
     base, route0 = run("0")
     assert route == "conv_x3<64,64,f16x3,ksplit>" and route0 != route, (route, route0)
     assert torch.equal(sp, sp2)
-    # the last split of each tile reducing in-kernel (DDMI_X3_SPLIT_FUSE=1): the reduce launch's order and expressions
-    monkeypatch.setenv("DDMI_X3_SPLIT_FUSE", "1")
-    fu, _ = run("2")
-    fu2, _ = run("2")
-    monkeypatch.delenv("DDMI_X3_SPLIT_FUSE")
-    monkeypatch.setenv("DDMI_X3_RED_LOOP", "1")  # the runtime-S reduce loop: same order, same bits
-    lp, _ = run("2")
-    monkeypatch.delenv("DDMI_X3_RED_LOOP")
-    assert torch.equal(lp, sp)
-    assert torch.equal(fu, fu2)
-    close(fu.permute(0, 3, 1, 2), sp.permute(0, 3, 1, 2).double(), 1e-6)
     ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), s, p) + r.double())
     close(sp.permute(0, 3, 1, 2), ref, 3e-5)
     close(base.permute(0, 3, 1, 2), ref, 3e-5)
-
-
-@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s", [
-    (64, 320, 1, 512, 2048, 1, 1),   # GPT MLP-up at C = 512 (256 x 256 tiles)
-    (64, 320, 1, 512, 1536, 1, 1),   # GPT qkv at C = 512
-    (64, 32, 128, 128, 256, 3, 2),   # image layer-3 stride-2 3x3 (generic K walk)
-    (40, 160, 2, 520, 768, 1, 1),    # ragged K (520 = 32 x 16 + 8) and M
-])
-def test_conv_x5_deep_ring_is_bit_identical(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
-    """conv_x5's opt-in deep-ring form (DDMI_X5_DEEP=1, read per dispatch: 16-deep K chunks in 4 stages at
-    256 x 256 tiles) runs the same MFMA sequence as the 32-deep 2-stage form: bit-identical outputs."""
-    p = k // 2
-    x = rnd(B, Cin, H, W, seed=81)
-    w = rnd(Cout, Cin, k, k, seed=82, scale=1.0 / np.sqrt(Cin * k * k))
-    b = rnd(Cout, seed=83)
-    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    r = rnd(B, Cout, Ho, Wo, seed=84)
-    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
-
-    def run(deep):
-        monkeypatch.setenv("DDMI_X5_DEEP", deep)
-        out = torch.empty(B, Ho, Wo, Cout, device=DEV)
-        flags = torch.zeros(1, dtype=torch.int32, device=DEV)
-        ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
-                               out.data_ptr(), Cout, k, k, s, p, 1, 0, flags.data_ptr(), None), gpu)
-        assert int(flags.item()) == 0
-        return out, gpu.dd_op_last_kernel().decode()
-
-    deep, route = run("1")
-    base, route0 = run("0")
-    assert route == "conv_x5<256,256,k16>" and route0 == "conv_x5<256,256>", (route, route0)
-    assert torch.equal(deep, base)
-    if B * Ho * Wo * Cout * Cin * k * k < 6e9:  # the fp64 CPU reference only where it takes seconds
-        ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), s, p) + r.double())
-        close(deep.permute(0, 3, 1, 2), ref, 3e-5)
-
-
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [
-    (8, 64, 64, 32, 200),     # Cin = 32 (one K chunk), ragged N: the case the round-4 form failed
-    (32, 20, 36, 64, 256),    # ragged tiles in H and W, two chunks
-    (64, 32, 128, 128, 128),  # image layer2 3x3
-    (64, 16, 64, 256, 256),   # image layer3 3x3
-    (64, 32, 32, 128, 128),   # LiDAR layer2
-])
-def test_conv2d_f16x3_two_per_cu_form(gpu, monkeypatch, B, H, W, Cin, Cout):
-    """conv_x6's BN = 128 form as two 8-wave workgroups per CU on 8 x 16 tiles (one halo buffer, 128 VGPRs,
-    unpipelined fragments; DDMI_X6_CFG=3, read per dispatch) against PyTorch-CPU fp64 at the f16x3 bar."""
-    monkeypatch.setenv("DDMI_X6_CFG", "3")
-    x = rnd(B, Cin, H, W, seed=71)
-    w = rnd(Cout, Cin, 3, 3, seed=72, scale=1.0 / np.sqrt(Cin * 9))
-    b = rnd(Cout, seed=73)
-    ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), 1, 1) + (r := rnd(B, Cout, H, W, seed=74)).double())
-    out = torch.empty(ref.permute(0, 2, 3, 1).shape, device=DEV)
-    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
-    xin, win, bin_, rin = g(x.permute(0, 2, 3, 1)), g(w.permute(0, 2, 3, 1)), g(b), g(r.permute(0, 2, 3, 1))
-    ok(gpu.dd_op_conv2d_x3(xin.data_ptr(), B, H, W, Cin, win.data_ptr(), bin_.data_ptr(), rin.data_ptr(),
-                           out.data_ptr(), Cout, 3, 3, 1, 1, 1, 0, flags.data_ptr(), None), gpu)
-    assert gpu.dd_op_last_kernel().decode() == "conv_x6<8,16,128,4,2>"
-    close(out.permute(0, 3, 1, 2), ref, 3e-5)
-    assert int(flags.item()) == 0
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p,res,route", [

@@ -483,17 +483,13 @@ def test_fused_token_pooling_matches_avgpool(gpu_model, seeded_sd, monkeypatch):
 
 def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
     """The gathered value_proj on the same inputs: the default kernel (value_proj.hip: compacted rows in 256-row
-    tiles, each tile as two 128-channel halves, K whole, the tile's 3 x 3-neighbourhood union staged once per
-    16-channel group), the same tiles gathered per (row, tap) (DDMI_VPROJ_UNION=0), the union form with every tile /
-    the larger-union tiles handed to the gathered fallback (DDMI_VPROJ_UMAX=0 / 600: bit-identical to the gathered
-    form on those tiles), the union form with its K split over the channel groups 1 / 4 / 8 ways (DDMI_VPROJ_USPLIT;
-    8 is this batch's default: the partials summed in split order by the last split; a step barrier at every step,
-    DDMI_VPROJ_BAR=1, is bit-identical to the default schedule's), its 256 x 256 form with the K split three / two / one ways
-    (DDMI_VPROJ_N=1, DDMI_VPROJ_SPLITS; the partials summed in split order by the last split), conv_x3 over the
-    compacted rows (DDMI_VALUE_SPLITK=0) and conv_x3 with one tile run per scene (+ DDMI_VALUE_COMPACT=0). The
-    conv_x3 forms evaluate every row with the same dot products in the same K order wherever its tile sits:
-    bit-identical, and so are the unsplit value_proj.hip forms. The K-split forms differ by summation order only:
-    every live row within 1e-5 relative, trajectories within 1e-5."""
+    tiles, each tile as two 128-channel halves, the tile's 3 x 3-neighbourhood union staged once per 16-channel
+    group, its K split over the channel groups 8 ways at this batch), the same tiles gathered per (row, tap)
+    (DDMI_VPROJ_UNION=0), the union form with every tile / the larger-union tiles handed to the gathered fallback
+    (DDMI_VPROJ_UMAX=0 / 600: bit-identical to the gathered form on those tiles), the union form unsplit and split 4
+    ways (DDMI_VPROJ_USPLIT; the partials summed in split order by the last split), and conv_x3 over the compacted
+    rows (DDMI_VALUE_SPLITK=0). The forms differ by summation order only: every live row within 1e-5 relative,
+    trajectories within 1e-5."""
     from diffusiondrive_amd.model import DiffusionDriveModel
     from diffusiondrive_amd.weights import synthetic_inputs
     B = 6
@@ -528,7 +524,7 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
 
     gpu_model.set_gemm_mode("f16x3")
     try:
-        runs = {"nhalf2": run(gpu_model, profile=True)}  # the default: two 128-channel halves, no K split
+        runs = {"default": run(gpu_model, profile=True)}
     finally:
         gpu_model.set_profiling(False)
         gpu_model.set_gemm_mode("fp32")
@@ -537,39 +533,24 @@ def test_value_proj_variants_agree(gpu_model, seeded_sd, monkeypatch):
     runs["union_fb_some"] = fresh(DDMI_VPROJ_UMAX="600")
     runs["union_split1"] = fresh(DDMI_VPROJ_USPLIT="1")
     runs["union_split4"] = fresh(DDMI_VPROJ_USPLIT="4")
-    runs["union_split8"] = fresh(DDMI_VPROJ_USPLIT="8")
-    runs["union_split1_bar1"] = fresh(DDMI_VPROJ_USPLIT="1", DDMI_VPROJ_BAR="1")
-    runs["splitk3"] = fresh(DDMI_VPROJ_N="1")
-    runs["splitk2"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="2")
-    runs["splitk1"] = fresh(DDMI_VPROJ_N="1", DDMI_VPROJ_SPLITS="1")
     runs["x3"] = fresh(DDMI_VALUE_SPLITK="0")
-    runs["x3_per_scene"] = fresh(DDMI_VALUE_SPLITK="0", DDMI_VALUE_COMPACT="0")
     ref_out, ref = runs["x3"]
-    lines = ["== gathered value_proj: value_proj.hip (3 / 2 / 1 K splits; two 128-channel N halves) vs conv_x3 "
-             "(compacted / per scene)"]
+    forms = ("default", "gathered2", "union_fb_some", "union_split1", "union_split4")
+    lines = ["== gathered value_proj: value_proj.hip forms vs conv_x3 over the compacted rows"]
     for k in names:
         rows = ref[k][0]
         live = rows >= 0
-        assert np.array_equal(rows, runs["x3_per_scene"][1][k][0]), k
-        assert np.array_equal(ref[k][1][live], runs["x3_per_scene"][1][k][1][live]), k
         # every tile handed to the fallback: exactly the gathered two-half form
         assert np.array_equal(runs["union_fb_all"][1][k][1][live], runs["gathered2"][1][k][1][live]), k
-        for v in ("splitk3", "splitk2", "splitk1", "nhalf2", "gathered2", "union_fb_some", "union_split1",
-                  "union_split4", "union_split8"):
+        for v in forms:
             got = runs[v][1][k]
             assert np.array_equal(rows, got[0]), (v, k)
             r = ref[k][1][live]
             err = float(np.abs(got[1][live] - r).max() / max(1.0, np.abs(r).max()))
             lines.append(f"  {k} {v}: {int(live.sum())} live rows, max rel err vs conv_x3 {err:.3e}")
             assert err <= 1e-5, (v, k, err)
-    # the barrier schedule changes no arithmetic
-    assert np.array_equal(runs["union_split1"][0], runs["union_split1_bar1"][0])
-    for k in names:
-        assert np.array_equal(runs["union_split1"][1][k][1], runs["union_split1_bar1"][1][k][1]), k
-    assert np.array_equal(ref_out, runs["x3_per_scene"][0])
     assert np.array_equal(runs["union_fb_all"][0], runs["gathered2"][0])
-    for v in ("splitk3", "splitk2", "splitk1", "nhalf2", "gathered2", "union_fb_some", "union_split1", "union_split4",
-              "union_split8"):
+    for v in forms:
         l2 = waypoint_l2(runs[v][0], ref_out)
         lines.append(f"  trajectory waypoint L2 {v} vs conv_x3 {l2:.3e}")
         assert l2 <= 1e-5, (v, l2)
@@ -710,50 +691,6 @@ def test_small_batch_forms_at_their_boundary(seeded_sd, B):
     assert l2 <= WAYPOINT_L2_TOL
 
 
-def test_fused_basicblock_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
-    """Layer 1 of both trunks (stride-1 64-channel BasicBlocks) runs as one launch per block (basicblock.hip: conv1's
-    output for the 18 x 18 pixels conv2 reads kept in LDS): the stage outputs, the GPT tokens pooled from the last
-    block and the whole forward are bit-identical to the two conv_x6 launches per block (the default; DDMI_BB_FUSE=1
-    enables the fused form) - the same products, K order and epilogue expressions, the intermediate split as conv_x6
-    splits its halo."""
-    from diffusiondrive_amd.model import DiffusionDriveModel
-    from diffusiondrive_amd.weights import synthetic_inputs
-    B = 3
-    inp = synthetic_inputs(B, 59)
-    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
-    nz = torch.from_numpy(inp["noise"]).cuda()
-    taps = ("img_s0_a", "lid_s0_a", "img_s0_b", "lid_s0_b")
-
-    def run(m):
-        m.set_profiling(True)
-        m.reset_stats()
-        out = m.forward(feats, noise=nz, modes=True)
-        launches = m.kernel_stats("basicblock")["launches"]
-        m.set_profiling(False)
-        res = {k: v.cpu().numpy() for k, v in out.items()}
-        res.update({t: m.tap(t).cpu().numpy() for t in taps})
-        return res, launches
-
-    gpu_model.set_gemm_mode("f16x3")
-    try:
-        ref, n_ref = run(gpu_model)
-    finally:
-        gpu_model.set_gemm_mode("fp32")
-    monkeypatch.setenv("DDMI_BB_FUSE", "1")
-    m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
-    try:
-        fused, n_fused = run(m)
-        replay = {k: v.cpu().numpy() for k, v in m.forward(feats, noise=nz, modes=True).items()}
-    finally:
-        m.close()
-    assert n_fused == 6 and n_ref == 0, (n_fused, n_ref)
-    for k in ref:
-        n = min(fused[k].size, ref[k].size)
-        assert np.array_equal(fused[k].reshape(-1)[:n], ref[k].reshape(-1)[:n]), k
-    for k in replay:
-        assert np.array_equal(replay[k], ref[k]), k  # the captured graph as well
-
-
 @pytest.mark.gpu
 def test_decoder_query_groups_are_bit_identical(gpu_model, seeded_sd, monkeypatch):
     """decoder_mk splits a scene's 20 modes over 4 (or 2) workgroups of 5 (10) queries (the default while B x 4 fits
@@ -782,40 +719,6 @@ def test_decoder_query_groups_are_bit_identical(gpu_model, seeded_sd, monkeypatc
         for o in outs:
             for k in ref[0]:
                 assert np.array_equal(o[k], ref[0][k]), (g, k)
-
-
-@pytest.mark.gpu
-def test_stage_chunk_is_bit_identical(gpu_model, seeded_sd, monkeypatch):
-    """Layer 1 of each trunk in chunks of scenes whose maps fit the memory-side cache (opt-in DDMI_S0_CHUNK_MB, e.g.
-    72 MB: 16 camera scenes), every chunk through all of the stage's blocks before the next: the same convs on the
-    same pixels, so the stage outputs, the GPT tokens pooled from them and the forward are bit-identical to the
-    whole-batch stage (the default, DDMI_S0_CHUNK_MB=0). B = 20 with 8 MB chunks: uneven chunks (2 scenes each, camera) and a
-    LiDAR stage that chunks too."""
-    from diffusiondrive_amd.model import DiffusionDriveModel
-    from diffusiondrive_amd.weights import synthetic_inputs
-    B = 20
-    inp = synthetic_inputs(B, 67)
-    feats = {k: torch.from_numpy(inp[k]).cuda() for k in ("camera_feature", "lidar_feature", "status_feature")}
-    nz = torch.from_numpy(inp["noise"]).cuda()
-    taps = ("img_s0_a", "lid_s0_a", "img_s0_b", "lid_s0_b")
-
-    def run(mb):
-        monkeypatch.setenv("DDMI_S0_CHUNK_MB", mb)
-        m = DiffusionDriveModel(state_dict=seeded_sd, device=0, gemm="f16x3")
-        try:
-            outs = [{k: v.cpu().numpy() for k, v in m.forward(feats, noise=nz, modes=True).items()} for _ in range(2)]
-            outs[0].update({t: m.tap(t).cpu().numpy() for t in taps})
-        finally:
-            m.close()
-        return outs
-
-    ref = run("0")
-    for mb in ("9", "72"):
-        got = run(mb)
-        for k in ref[0]:
-            assert np.array_equal(got[0][k], ref[0][k]), (mb, k)
-        for k in ref[1]:
-            assert np.array_equal(got[1][k], ref[1][k]), (mb, k)
 
 
 @pytest.mark.gpu
