@@ -72,14 +72,18 @@ constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread pe
 constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
 constexpr int LDS_BYTES = 2 * IMG_BYTES + NMT * 32 * SOP * 4;
 
-// One input channel (the LiDAR histogram, SRC_C = 1), opt-in (DDMI_STEM1=1, read per dispatch): K = 7 kh x 8 kw = 56 real taps (kw = 7 and kh = 7 zero) in 4
-// k16 steps instead of 14 over the 4-channel pixels. A lane's 8 halves are 8 consecutive input columns of one row,
-// which start at an even column 2 lx: the patch is held as 4 copies shifted by 0, 2, 4, 6 columns, so the read for
-// stem column lx comes from copy lx & 3 at the 16-B aligned column 8 (lx >> 2). Copies 2368 B apart (= 64 mod 256):
-// the 16 lanes of a ds_read_b128 group in one stem row fall on 16 distinct 4-bank groups.
-// Not the default: the same products summed in another K order move the B = 64 golden's per-mode poses of an
-// intermediate layer to 1.09e-4 against the 1e-4 bar (1.3e-5 with the 4-channel order; profiles/round4_t_stem1.txt,
-// reproduced in round 5) - the per-mode outputs amplify a rounding-level change of the LiDAR stem by ~10^3.
+// One input channel (the LiDAR histogram, SRC_C = 1; the default since round 6, DDMI_STEM1=0 takes the 4-channel form,
+// read per dispatch): K = 7 kh x 8 kw = 56 real taps (kw = 7 and kh = 7 zero) in 4 k16 steps instead of 14 over the
+// 4-channel pixels. A lane's 8 halves are 8 consecutive input columns of one row, which start at an even column 2 lx:
+// the patch is held as 4 copies shifted by 0, 2, 4, 6 columns, so the read for stem column lx comes from copy lx & 3
+// at the 16-B aligned column 8 (lx >> 2). Copies 2368 B apart (= 64 mod 256): the 16 lanes of a ds_read_b128 group in
+// one stem row fall on 16 distinct 4-bank groups.
+// The f16x3 cross products (al bh, ah bl) accumulate apart from ah bh and are added once at the end. With all three
+// in one accumulator (rounds 4-5) the B = 64 golden's per-mode headings of one scene moved to 1.1e-4 against the 1e-4
+// bar although the pooled stem map was within 2e-7 of the 4-channel form's and 1.6e-7 of fp64 (as accurate as it);
+// apart, every per-mode pose is within 1.4e-5 of the golden, as with the 4-channel form (profiles/round6_stem1.md,
+// tools/debug/stem1_diag.py, tools/micro/stem_prec.py). The reference's own per-mode response to a summation-order
+// change of the LiDAR stem (the oracle with that conv in fp64) is 0.7-1.3e-5 (tests/test_conditioning.py).
 constexpr int KS1 = 4;
 constexpr int IH1 = IH + 1;                        // + a zero row for the kh = 7 padding tap
 constexpr int IP1 = 40;                            // halves per copy row (80 B: 16-B aligned rows)
@@ -273,9 +277,9 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
       const int base = (2 * ly) * IP + 2 * lx + 2 * hl;  // input pixel of (kh 0, kw 2h)
       // one channel: copy lx & 3, row 2 ly + hl (+ 2 s), 16-B aligned column 8 (lx >> 2)
       const int base1 = (lx & 3) * CB1 + ((2 * ly + hl) * IP1 + 8 * (lx >> 2)) * 2;
-      sp_f16 acc;
+      sp_f16 acc, acc2;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
 #pragma unroll
       for (int s = 0; s < KSN; ++s) {
         const int off = C1 ? base1 + s * 2 * IP1 * 2 : (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
@@ -285,10 +289,19 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
                                                         acc, 0, 0, 0);
         } else {
           const sp_h8 al = *reinterpret_cast<const sp_h8*>(in_lo + off);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+          if constexpr (C1) {  // the cross products in an accumulator of their own (header: one channel)
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc2, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc2, 0, 0, 0);
+          } else {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+          }
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
         }
+      }
+      if constexpr (C1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
       }
       // C/D layout: column (channel) li, row (pixel) (r & 3) + 8 (r >> 2) + 4 hl
 #pragma unroll
@@ -364,7 +377,7 @@ bool launch_stem_pool(const ConvArgs& a, float* pool_out, int Hp, int Wp, hipStr
   const int grid = ntiles < per_cu * cus ? ntiles : per_cu * cus;
   const int c = src ? src_c : 0;
   const char* oe = getenv("DDMI_STEM1");
-  const bool one = c == 1 && oe && atoi(oe) != 0;
+  const bool one = c == 1 && !(oe && atoi(oe) == 0);
   static std::atomic<uint64_t> attr[2][5];
   auto go = [&](auto kern, int c) {
     const int lds = (c == 1 && one) ? LDS1_BYTES : LDS_BYTES;

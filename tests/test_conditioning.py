@@ -1,25 +1,41 @@
 """CPU: how sensitive the reference computation itself is at the bench workload (B = 64, seed 1234).
 
-The oracle (the CPU restatement pinned to the reference goldens) runs twice, the second time with the camera
-input perturbed by one fp32 ulp (2^-24 relative, seeded). The change of agent_states under that perturbation
-is the floor any fp32-class implementation can be held to; tests/test_parity_gpu.py's AGENT_TOL is tied to it
-(10x), and the north-star trajectory bar (1e-4 waypoint L2) must stay far above the trajectory's own change.
+The oracle (the CPU restatement pinned to the reference goldens) runs unperturbed and with one input or one
+summation order changed:
+
+* the camera input perturbed by one fp32 ulp (2^-24 relative, seeded): the change of agent_states is the floor any
+  fp32-class implementation can be held to; tests/test_parity_gpu.py's AGENT_TOL is tied to it (10x), and the
+  north-star trajectory bar (1e-4 waypoint L2) must stay far above the trajectory's own change;
+* the LiDAR stem conv (transfuser_backbone.py:175-185) evaluated in fp64 and rounded once (a summation-order change
+  of exactly the kind a different kernel K order makes), the LiDAR input perturbed by one fp32 ulp, and one LiDAR
+  histogram bin per scene raised by one point (0.2): the per-(step, layer) poses' response is the basis of the
+  per-mode bar MODE_TOL (1e-4) - a rounding-level change of the LiDAR stem moves them by ~1e-5, so a kernel form that
+  moves them by 1e-4 carries a defect of its own (profiles/round6_stem1.md).
 """
 import numpy as np
 import pytest
 import torch
 
-from test_parity_gpu import AGENT_TOL, WAYPOINT_L2_TOL
+from test_parity_gpu import AGENT_TOL, MODE_TOL, WAYPOINT_L2_TOL
+
+REGS = [f"reg_s{s}l{l}" for s in range(2) for l in range(2)]
 
 
-@pytest.mark.timeout(300)
-def test_agent_head_conditioning_bounds_agent_tol(seeded_sd):
+@pytest.fixture(scope="module")
+def bench_case(seeded_sd):
     from diffusiondrive_amd.weights import synthetic_inputs
-    from oracle.model import OracleModel
+    from oracle.model import OracleModel, Taps
     torch.set_num_threads(8)
     m = OracleModel(seeded_sd)
     inp = synthetic_inputs(64, 1234)
-    base = m.forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"], inp["noise"])
+    taps = Taps()
+    base = m.forward(inp["camera_feature"], inp["lidar_feature"], inp["status_feature"], inp["noise"], taps=taps)
+    return m, inp, base, taps
+
+
+@pytest.mark.timeout(300)
+def test_agent_head_conditioning_bounds_agent_tol(bench_case):
+    m, inp, base, _ = bench_case
     rng = np.random.default_rng(0)
     cam = (inp["camera_feature"] * (1 + 2.0**-24 * rng.standard_normal(inp["camera_feature"].shape))).astype(np.float32)
     pert = m.forward(cam, inp["lidar_feature"], inp["status_feature"], inp["noise"])
@@ -29,3 +45,44 @@ def test_agent_head_conditioning_bounds_agent_tol(seeded_sd):
     assert 1e-5 < d_agent, "the agent head is no longer ill-conditioned: tighten AGENT_TOL"
     assert AGENT_TOL <= 20 * d_agent, (AGENT_TOL, d_agent)
     assert d_traj < 0.1 * WAYPOINT_L2_TOL
+
+
+@pytest.mark.timeout(600)
+def test_lidar_stem_conditioning_bounds_mode_tol(bench_case, monkeypatch):
+    """The per-mode poses' response to the LiDAR stem's summation order and to a one-ulp / one-bin LiDAR change
+    (printed per (step, layer)); the summation-order and one-ulp responses must sit well below MODE_TOL."""
+    import oracle.model as om_mod
+    from oracle.model import Taps
+    m, inp, base, tb = bench_case
+    args = (inp["camera_feature"], None, inp["status_feature"], inp["noise"])
+
+    def run(lid):
+        t = Taps()
+        m.forward(args[0], lid, args[2], args[3], taps=t, heads=False)
+        return {k: float((t[k] - tb[k]).abs().max()) for k in REGS}
+
+    orig = om_mod.trunk_stem
+
+    def stem64(x, sd, p):
+        if "lidar" not in p:
+            return orig(x, sd, p)
+        y = torch.nn.functional.conv2d(x.double(), sd[p + ".conv1.weight"].double(), None, 2, 3).float()
+        return torch.relu(om_mod.bn(y, sd, p + ".bn1"))
+
+    monkeypatch.setattr(om_mod, "trunk_stem", stem64)
+    d_order = run(inp["lidar_feature"])
+    monkeypatch.setattr(om_mod, "trunk_stem", orig)
+    rng = np.random.default_rng(0)
+    lid = inp["lidar_feature"]
+    d_ulp = run((lid * (1 + 2.0**-24 * rng.standard_normal(lid.shape))).astype(np.float32))
+    lid_bin = lid.copy()
+    for b in range(lid.shape[0]):
+        y, x = rng.integers(0, lid.shape[2]), rng.integers(0, lid.shape[3])
+        lid_bin[b, 0, y, x] = min(1.0, lid_bin[b, 0, y, x] + 0.2)
+    d_bin = run(lid_bin.astype(np.float32))
+    for name, d in (("LiDAR stem in fp64 (summation order)", d_order), ("LiDAR one ulp", d_ulp),
+                    ("LiDAR one bin (+1 point per scene)", d_bin)):
+        print(f"{name}: " + ", ".join(f"{k} {v:.3e}" for k, v in d.items()))
+    assert max(d_order.values()) < 0.3 * MODE_TOL, d_order
+    assert max(d_ulp.values()) < 0.3 * MODE_TOL, d_ulp
+    assert max(d_bin.values()) > MODE_TOL  # a real input change is visible far above the bar
