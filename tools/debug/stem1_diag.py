@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The one-channel LiDAR stem (the default; DDMI_STEM1=0 = the 4-channel form) against the 4-channel form on the bench's B = 64 golden batch (GPU):
+"""The one-channel LiDAR stem (DDMI_STEM1=1) against the 4-channel form on the bench's B = 64 golden batch (GPU):
 the pooled LiDAR stem map, the LiDAR trunk taps, and every per-(step, layer) reg / cls against the reference golden,
 with the (scene, mode) where each reg error peaks. Each form on a fresh handle (the knob is read per dispatch)."""
 import os

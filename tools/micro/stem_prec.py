@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Precision of the fused stem forms against fp64 (GPU): the 4-channel-pixel form (DDMI_STEM1=0, K = 224) and the
-one-channel LiDAR form (the default, K = 64, f16x3 cross products in an accumulator of their own). Round 6 ran it
+one-channel LiDAR form (DDMI_STEM1=1, K = 64, f16x3 cross products in an accumulator of their own). Round 6 ran it
 with a third form, the one-channel form with one accumulator (profiles/round6_stem1.md). Inputs: a LiDAR-like histogram (multiples of 0.2, ~90 % zeros) and dense |N(0,1)|; seeded weights.
 Prints max / mean abs error over the pooled map, relative to max |ref|, and the bias (mean signed error)."""
 import os
