@@ -12,7 +12,7 @@ done
 timeout -k 10 400 env DDMI_STREAM_POOL=0 python -u -m pytest tests/test_runner.py tests/test_inflight_gpu.py \
   tests/test_agent.py -v -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/${T}_order.log 2>&1
 rc=$?; echo "[order] rc=$rc"; tail -2 gpurun_out/${T}_order.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 900 python -u -m pytest tests -v -m gpu -x -rf --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -x -rf --durations=30 --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1
 rc=$?; echo "[suite] rc=$rc"; tail -3 gpurun_out/${T}_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1
 rc=$?; echo "[smoke] rc=$rc"; tail -2 gpurun_out/${T}_smoke.log; [ $rc -ne 0 ] && exit $rc
