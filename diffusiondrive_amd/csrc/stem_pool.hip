@@ -29,6 +29,7 @@
 // Bound: MFMA (f16x3 ceiling 833 TF): 49 x 4 x 64 x 2 = 25 KFLOP per stem pixel, 1.17 x recompute,
 // 224 / 196 K padding; HBM traffic = the input once (+ halo re-reads) + the pooled map.
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 
@@ -49,10 +50,10 @@ typedef __bf16 sp_b4 __attribute__((ext_vector_type(4)));
 // 7 x 8 tile (255 stem pixels, one workgroup per CU; same-box bench A/B). (A 4 x 16 tile's 297 pixels made 10 M
 // tiles: 3 for half the waves, 2 for the rest.)
 constexpr int PH = 5, PW = 8;                      // pooled outputs per tile
-constexpr int SH = 2 * PH + 1, SW = 2 * PW + 1;    // stem pixels per tile (15 x 17)
-constexpr int NSP = SH * SW;                       // 255
-constexpr int NMT = (NSP + 31) / 32;               // 8 M tiles
-constexpr int IH = 4 * PH + 7, IW = 4 * PW + 8;    // input pixels per tile (35 x 40; the last column feeds
+constexpr int SH = 2 * PH + 1, SW = 2 * PW + 1;    // stem pixels per tile (11 x 17)
+constexpr int NSP = SH * SW;                       // 187
+constexpr int NMT = (NSP + 31) / 32;               // 6 M tiles
+constexpr int IH = 4 * PH + 7, IW = 4 * PW + 8;    // input pixels per tile (27 x 40; the last column feeds
                                                    // only the zero kw = 7 tap, but must be finite)
 // LDS pitch in pixels: even (a k-step's 2-pixel fragment is 16-B aligned at every kernel row) and = 2 (mod 16): a
 // lane's fragment slot is then p + ly (mod 16) for stem pixel p = 17 ly + lx, so a 16-lane ds_read_b128 group
@@ -68,6 +69,8 @@ constexpr int SOP = 64;                            // stem tile pitch (floats): 
                                                    // consecutive channels either way
 constexpr int NT = 256;                            // threads (4 waves; two workgroups per CU)
 constexpr int MSTEP = NT / 128;                    // M-tile stride of a wave (waves = 2 N halves x MSTEP)
+constexpr int MPW = NMT / MSTEP;                   // M tiles per wave (3)
+static_assert(MPW * MSTEP == NMT, "the M tiles split evenly over the waves");
 constexpr int ILD = (IH * IW + NT - 1) / NT;       // input pixels per thread per tile
 constexpr int IMG_BYTES = IH * IP * 8;             // one fp16 input image
 constexpr int LDS_BYTES = 2 * IMG_BYTES + NMT * 32 * SOP * 4;
@@ -94,6 +97,12 @@ constexpr int IMG1_BYTES = 4 * CB1;                // the 4 copies of one fp16 i
 constexpr int ILD1 = (IH * IW + NT - 1) / NT;      // input pixels per thread per tile
 constexpr int LDS1_BYTES = 2 * IMG1_BYTES + NMT * 32 * SOP * 4;
 
+// f(integral_constant<U>) for U in the sequence, in order (a compile-time unrolled loop)
+template <class F, int... U>
+__device__ inline void sp_for_each(F&& f, std::integer_sequence<int, U...>) {
+  (f(std::integral_constant<int, U>()), ...);
+}
+
 __device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
   hi = __builtin_convertvector(v, sp_h4);
   const sp_f4 r = v - __builtin_convertvector(hi, sp_f4);
@@ -104,7 +113,7 @@ __device__ inline void sp_split4(const sp_f4 v, sp_h4& hi, sp_h4& lo) {
 // tensor with SRC_C channels, whose address the kernel reads from *src (a device word the runtime sets per call
 // outside the captured graph), the missing channels zero - the same 4-channel pixels, without the transpose pass.
 template <int PREC, int SRC_C, int ONE = 0>
-__global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__ in, const float* const* src, int H,
+__global__ __launch_bounds__(NT, 2) void stem_pool_kernel(const float* __restrict__ in, const float* const* src, int H,
                                                        int W, int Hs, int Ws,
                                                        int Hp, int Wp, const uint16_t* __restrict__ wh,
                                                        const uint16_t* __restrict__ wl, int ldh,
@@ -166,7 +175,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
   }
   const float scl = wsinv[co] * alpha;
   const float bia = bias ? bias[co] : 0.f;
-  bool bad = false;
+  float nf = 0.f;  // NaN once any accumulator was non-finite
 
   auto tile_origin = [&](int t, int& b, int& py0, int& px0) {
     const int tx = t % tiles_x, t2 = t / tiles_x;
@@ -266,58 +275,94 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
   for (; t < ntiles; t += gridDim.x) {
     store_patch();
     __syncthreads();
-    if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x);  // lands under this tile's MFMAs
 
     int b, py0, px0;
     tile_origin(t, b, py0, px0);
     const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;
-    // ---- stem GEMM: wave (nt, mg) takes M tiles mg, mg + 4, mg + 8
-    for (int m = mg; m < NMT; m += MSTEP) {
-      const int p = min(m * 32 + li, NSP - 1);
+    // ---- stem GEMM: wave (nt, mg) takes M tiles mg, mg + 2, mg + 4, one after the other (one accumulator), each
+    // tile's 14 k16 steps then its epilogue into the LDS stem tile. The 42 (tile, step) units run as one unrolled
+    // sequence whose fragment reads are issued two units ahead (a ring of three fragment sets), across tile
+    // boundaries too, so every read lands under earlier MFMAs (or a tile's epilogue) instead of being waited for
+    // right before its own MFMAs. Per accumulator: the steps in order, the three products in the same order.
+    int abase[MPW];
+#pragma unroll
+    for (int i = 0; i < MPW; ++i) {
+      const int p = min((mg + MSTEP * i) * 32 + li, NSP - 1);
       const int ly = p / SW, lx = p - (p / SW) * SW;
-      const int base = (2 * ly) * IP + 2 * lx + 2 * hl;  // input pixel of (kh 0, kw 2h)
-      // one channel: copy lx & 3, row 2 ly + hl (+ 2 s), 16-B aligned column 8 (lx >> 2)
-      const int base1 = (lx & 3) * CB1 + ((2 * ly + hl) * IP1 + 8 * (lx >> 2)) * 2;
-      sp_f16 acc, acc2;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < KSN; ++s) {
-        const int off = C1 ? base1 + s * 2 * IP1 * 2 : (base + (s >> 1) * IP + 4 * (s & 1)) * 8;
-        const sp_h8 ah = *reinterpret_cast<const sp_h8*>(in_hi + off);
-        if constexpr (PREC == 1) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_b8, ah), __builtin_bit_cast(sp_b8, bh[s]),
-                                                        acc, 0, 0, 0);
-        } else {
-          const sp_h8 al = *reinterpret_cast<const sp_h8*>(in_lo + off);
-          if constexpr (C1) {  // the cross products in an accumulator of their own (header: one channel)
-            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc2, 0, 0, 0);
-            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc2, 0, 0, 0);
-          } else {
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
-          }
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
-        }
-      }
-      if constexpr (C1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
-      }
-      // C/D layout: column (channel) li, row (pixel) (r & 3) + 8 (r >> 2) + 4 hl
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int pr = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        if (pr < NSP) {
-          bad |= !__builtin_isfinite(acc[r]);
-          const int sy = sy0 + pr / SW, sx = sx0 + pr % SW;
-          float v = fmaxf(acc[r] * scl + bia, 0.f);
-          if ((unsigned)sy >= (unsigned)Hs || (unsigned)sx >= (unsigned)Ws) v = 0.f;
-          so[pr * SOP + co] = v;
-        }
-      }
+      // 4 channels: input pixel of (kh 0, kw 2h); one channel: copy lx & 3, row 2 ly + hl (+ 2 s), 16-B aligned column
+      // 8 (lx >> 2)
+      abase[i] = C1 ? (lx & 3) * CB1 + ((2 * ly + hl) * IP1 + 8 * (lx >> 2)) * 2
+                    : ((2 * ly) * IP + 2 * lx + 2 * hl) * 8;
     }
+    constexpr int NU = MPW * KSN, PD = 2;  // units, prefetch distance
+    sp_h8 fh[PD + 1], fl[PD + 1];
+    auto issue = [&](auto U) {
+      constexpr int u = decltype(U)::value;
+      if constexpr (u < NU) {
+        constexpr int i = u / KSN, st = u % KSN;
+        constexpr int so_ = C1 ? st * 2 * IP1 * 2 : ((st >> 1) * IP + 4 * (st & 1)) * 8;
+        fh[u % (PD + 1)] = *reinterpret_cast<const sp_h8*>(in_hi + abase[i] + so_);
+        if constexpr (PREC == 0) fl[u % (PD + 1)] = *reinterpret_cast<const sp_h8*>(in_lo + abase[i] + so_);
+      }
+    };
+    sp_f16 acc, acc2;
+    auto unit = [&](auto U) {
+      constexpr int u = decltype(U)::value;
+      constexpr int i = u / KSN, st = u % KSN, f = u % (PD + 1);
+      if constexpr (st == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
+      }
+      issue(std::integral_constant<int, u + PD>());
+      __builtin_amdgcn_sched_barrier(0);  // the reads of unit u + PD go out ahead of this unit's MFMAs
+      if constexpr (PREC == 1) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_b8, fh[f]), __builtin_bit_cast(sp_b8, bh[st]),
+                                                      acc, 0, 0, 0);
+      } else if constexpr (C1) {  // the cross products in an accumulator of their own (header: one channel)
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[f], bh[st], acc2, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[f], bl[st], acc2, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[f], bh[st], acc, 0, 0, 0);
+      } else {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[f], bh[st], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[f], bl[st], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[f], bh[st], acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (st == KSN - 1) {
+        if constexpr (C1) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
+        }
+        // epilogue of tile i into the LDS stem tile. C/D layout: column (channel) li, row (pixel) (r & 3) + 8 (r >> 2) +
+        // 4 hl. A non-finite accumulator turns the running fma(acc, 0, nf) into NaN (one fma per value instead of a class
+        // test; the padding rows of the last M tile are clamped to pixel NSP - 1, so finite). Rows NSP..191 of the last
+        // M tile are written and never read.
+        float* sob = so + ((mg + MSTEP * i) * 32 + 4 * hl) * SOP + co;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          nf = __builtin_fmaf(acc[r], 0.f, nf);
+          sob[((r & 3) + 8 * (r >> 2)) * SOP] = fmaxf(acc[r] * scl + bia, 0.f);
+        }
+      }
+    };
+    issue(std::integral_constant<int, 0>());
+    issue(std::integral_constant<int, 1>());
+    sp_for_each(unit, std::make_integer_sequence<int, NU>());
+    // the next tile's input patch: lands under this tile's pool (issued after the MFMAs, so its registers are not live
+    // beside the fragments)
+    if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x);
     __syncthreads();
+    // tiles at the map's edge: the stem pixels outside the map become 0 (every pool window holds at least one real
+    // pixel, all >= 0 after the ReLU, so 0 stands in for the pool's -inf padding)
+    if (sy0 < 0 || sx0 < 0 || sy0 + SH > Hs || sx0 + SW > Ws) {
+      for (int i = tid; i < NSP * 16; i += NT) {
+        const int pr = i >> 4, q = i & 15;
+        const int sy = sy0 + pr / SW, sx = sx0 + pr % SW;
+        if ((unsigned)sy >= (unsigned)Hs || (unsigned)sx >= (unsigned)Ws)
+          *reinterpret_cast<sp_f4*>(so + pr * SOP + 4 * q) = (sp_f4){0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();
+    }
     // ---- 3 x 3 / 2 max pool over the stem tile: (pooled pixel, channel quad) items
     for (int i = tid; i < PH * PW * 16; i += NT) {
       const int q = i & 15, pp = i >> 4;
@@ -334,15 +379,11 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const float* __restrict__
           mx.z = fmaxf(mx.z, v.z);
           mx.w = fmaxf(mx.w, v.w);
         }
-#ifdef DDMI_NT2  // experiment build (DDMI_BUILD_VARIANT=nt2): nontemporal pooled-map stores
-      if (gy < Hp && gx < Wp) __builtin_nontemporal_store(mx, reinterpret_cast<sp_f4*>(out + (((int64_t)b * Hp + gy) * Wp + gx) * 64 + 4 * q));
-#else
       if (gy < Hp && gx < Wp) *reinterpret_cast<sp_f4*>(out + (((int64_t)b * Hp + gy) * Wp + gx) * 64 + 4 * q) = mx;
-#endif
     }
     __syncthreads();  // the next tile overwrites the patch and the stem tile
   }
-  if (bad && flags) atomicOr(flags, (unsigned)DD_NUM_F16_OVERFLOW);
+  if (!__builtin_isfinite(nf) && flags) atomicOr(flags, (unsigned)DD_NUM_F16_OVERFLOW);
 }
 
 }  // namespace
