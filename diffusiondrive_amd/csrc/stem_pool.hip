@@ -270,9 +270,16 @@ __global__ __launch_bounds__(NT, 2) void stem_pool_kernel(const float* __restric
     }
   };
 
-  int t = blockIdx.x;
-  if (t < ntiles) load_patch(t);
-  for (; t < ntiles; t += gridDim.x) {
+  // XCD-aware tile walk: the workgroups of one XCD (blockIdx % 8) take one contiguous eighth of the tiles, 64 (grid / 8)
+  // consecutive tiles at a time, so the input halos that neighbouring tiles share are read into the same L2. (A grid
+  // that is not a multiple of 8 walks the tiles with the grid stride.)
+  const int G = gridDim.x;
+  const bool xcd = G % 8 == 0;
+  const int xq = (ntiles + 7) / 8, xb = xcd ? (int)(blockIdx.x % 8) * xq : 0, xe = xcd ? min(xb + xq, ntiles) : ntiles;
+  const int xs = xcd ? G / 8 : G;
+  int t = xb + (xcd ? (int)blockIdx.x / 8 : (int)blockIdx.x);
+  if (t < xe) load_patch(t);
+  for (; t < xe; t += xs) {
     store_patch();
     __syncthreads();
 
@@ -350,7 +357,7 @@ __global__ __launch_bounds__(NT, 2) void stem_pool_kernel(const float* __restric
     sp_for_each(unit, std::make_integer_sequence<int, NU>());
     // the next tile's input patch: lands under this tile's pool (issued after the MFMAs, so its registers are not live
     // beside the fragments)
-    if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x);
+    if (t + xs < xe) load_patch(t + xs);
     __syncthreads();
     // tiles at the map's edge: the stem pixels outside the map become 0 (every pool window holds at least one real
     // pixel, all >= 0 after the ReLU, so 0 stands in for the pool's -inf padding)
