@@ -55,6 +55,9 @@ __device__ inline x5i4 rsrc5a(const void* p) {
   r.y = (int)((uint32_t)(a >> 32) & 0xffffu);  // stride 0
   r.z = (int)kOOB5;                             // num_records: offsets >= 2^31 read as zero
   r.w = 0x00020000;
+  // wave-uniform by construction; readfirstlane keeps it in SGPRs for the "s" asm operands
+  r.x = __builtin_amdgcn_readfirstlane(r.x);
+  r.y = __builtin_amdgcn_readfirstlane(r.y);
   return r;
 }
 
@@ -478,6 +481,7 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
     if (m256 < 256) return false;
     launch_x5_cfg<4, 1, 2, 2, 3>(a, M, K, st);  // 256 x 64, 4 waves
   } else if (a.Cout > 128 && m256 * n256 >= 256) {
+    // (4 waves of 128 x 128 at one wave per SIMD, 512 VGPRs: 2.8x slower on the C = 512 qkv / MLP-up shapes, round 6)
     launch_x5_cfg<4, 2, 2, 4, 2>(a, M, K, st);  // 256 x 256, 8 waves
   } else if (a.Cout <= 128 && m256 * n128 >= 256) {
     launch_x5_cfg<4, 2, 2, 2, 3>(a, M, K, st);  // 256 x 128, 8 waves
