@@ -2,7 +2,7 @@
 # (MFMA busy, LDS conflicts, HBM read / write bytes, L2 hit) of both builds' stems (tools/micro/stem_ab.py, REPS=3)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
-OLD=$R/tools/micro/ab/libddmi_old.so
+OLD=$R/tools/micro/ab/old/libddmi.so
 DDMI_LIB=$OLD OUT=gpurun_out/r6p_old.json timeout -k 10 200 python tools/micro/stem_ab.py > gpurun_out/r6p_ab.log 2>&1 || { cat gpurun_out/r6p_ab.log; exit 1; }
 OUT=gpurun_out/r6p_new.json REF=gpurun_out/r6p_old.json timeout -k 10 200 python tools/micro/stem_ab.py >> gpurun_out/r6p_ab.log 2>&1 || { cat gpurun_out/r6p_ab.log; exit 1; }
 grep bit-identical gpurun_out/r6p_ab.log
