@@ -131,7 +131,7 @@ extern "C" int dd_x5_stamps_read(unsigned long long* h, int n) {
 // the stages fit (256 x 256: 4 stages of 32 KB, three chunks in flight instead of one), one k16 step and one
 // barrier per chunk. The MFMA sequence (k16 order, al*bh / ah*bl / ah*bh per step) is the same: bit-identical.
 template <int WM, int WN, int TM, int TN, int MODE, int NS, int PREC, int KCT = KC>
-__global__ __launch_bounds__(64 * WM * WN) void conv_x5_kernel(ConvArgs a, int M, int K, int n_tiles_m,
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 8 && TM * TN == 2) ? 4 : 1) void conv_x5_kernel(ConvArgs a, int M, int K, int n_tiles_m,
                                                                int n_tiles_n) {
   // MODE 1: Cin % KCT == 0 and KH*KW <= 32 (scalar tap walk, per-row tap masks); MODE 0: generic K.
   static_assert(KCT == 16 || KCT == 32, "K chunk");
@@ -473,6 +473,21 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   // short-K GEMMs with Cout = 512 / 1024 fill more of the chip with 192 x 256 tiles (proj C = 512: 61 -> 57 us,
   // MLP-up C = 256: 72 -> 65 us, C = 128: 30 -> 27 us); K = 2048 and the qkv shapes lose with the 3 x 2 wave
   // fragment layout (MLP-down 160 -> 162 us, qkv C = 512: 116 -> 145 us)
+  // 128 x 128 tiles at two workgroups per CU (8 waves of 32 x 64, 84 VGPRs, 66 KB LDS): one workgroup's epilogue
+  // and prologue run beside the other's K loop, and the grid is 4x finer than 256 x 256. Taken where it measured
+  // faster than the 256-wide tiles (tools/gpu_r6v.sh, profiles/round6/x5_t128_ab.md): the GPT MLP-up / MLP-down
+  // GEMMs (C = 256 / 512: -4 to -21 %) and the C = 512 proj, and the stride-2 3x3 convs except where the 256 x 256
+  // grid fills the chip in whole rounds (image layer 3 entry: +18 % there); the qkv GEMMs (Cout = 3 K) keep 256 x 256.
+  if (M >= 16384 && a.prec == 0 && a.Cin % KC == 0 && a.Cout % 128 == 0) {
+    const bool mlp = gemm && ((a.Cout >= 1024 && a.Cout % 1024 == 0 && K <= 512) || (K >= 1024 && a.Cout >= 256) ||
+                              (a.Cout == K && K >= 512));
+    const bool s2 = a.stride == 2 && a.KH == 3 && a.KW == 3 &&
+                    !(a.Cout >= 256 && (m256 * n256) % 256 == 0);
+    if (mlp || s2) {
+      launch_x5_cfg<4, 2, 1, 2, 2>(a, M, K, st);
+      return true;
+    }
+  }
   if (gemm && K <= 512 && (a.Cout == 512 || a.Cout == 1024) && M >= 16384) {
     launch_x5_cfg<2, 4, 3, 2, 2>(a, M, K, st);  // 192 x 256, 8 waves
     return true;

@@ -131,10 +131,10 @@ def test_conv2d_f16x3(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     (64, 8, 32, 512, 512, 3, 1, 1, True, True, "conv_x6<8,32,128,4,2>"),     # image layer4 (256 WGs of BN 128)
     (64, 32, 128, 128, 128, 3, 1, 1, True, True, "conv_x6<16,16,128,4,2>"),  # image layer2 3x3
     (64, 64, 256, 64, 64, 3, 1, 1, True, True, "conv_x6<16,16,64,4,1>"),     # image layer1 (4-wave, 2 WG / CU)
-    (64, 64, 256, 64, 128, 3, 2, 1, True, False, "conv_x5<256,128>"),        # image layer2 entry, 3x3 / s2
+    (64, 64, 256, 64, 128, 3, 2, 1, True, False, "conv_x5<128,128>"),        # image layer2 entry, 3x3 / s2 (2 WG / CU)
     (64, 32, 128, 128, 256, 3, 2, 1, True, False, "conv_x5<256,256>"),       # image layer3 entry, 3x3 / s2
-    (1, 160, 128, 512, 2048, 1, 1, 0, True, False, "conv_x5<256,256>"),      # GPT MLP-up at C = 512 (M = 20480)
-    (1, 160, 128, 2048, 512, 1, 1, 0, False, True, "conv_x5<256,256>"),      # GPT MLP-down at C = 512 (160 tiles)
+    (1, 160, 128, 512, 2048, 1, 1, 0, True, False, "conv_x5<128,128>"),      # GPT MLP-up at C = 512 (M = 20480)
+    (1, 160, 128, 2048, 512, 1, 1, 0, False, True, "conv_x5<128,128>"),      # GPT MLP-down at C = 512 (640 tiles)
     (1, 160, 128, 256, 768, 1, 1, 0, False, False, "conv_x5<256,256>"),      # GPT qkv at C = 256 (240 tiles)
     (1, 160, 128, 128, 384, 1, 1, 0, False, False, "conv_x5<256,128>"),      # GPT qkv at C = 128
     (1, 160, 128, 256, 256, 1, 1, 0, False, True, "conv_x3<64,64,f16x3>"),   # GPT proj at C = 256 (80 tiles)

@@ -7,7 +7,7 @@ import glob
 import os
 import sys
 
-SHAPES = [(1536, 512), (2048, 512), (512, 2048), (768, 256), (1024, 256)]
+SHAPES = [(1536, 512), (2048, 512), (512, 2048), (768, 256), (1024, 256), (512, 512), (256, 1024), (256, 256)]
 REPS = 13
 
 if "--parse" in sys.argv:
