@@ -477,13 +477,15 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   // and prologue run beside the other's K loop, and the grid is 4x finer than 256 x 256. Taken where it measured
   // faster than the 256-wide tiles (tools/gpu_r6v.sh, profiles/round6/x5_t128_ab.md): the GPT MLP-up / MLP-down
   // GEMMs (C = 256 / 512: -4 to -21 %) and the C = 512 proj, and the stride-2 3x3 convs except where the 256 x 256
-  // grid fills the chip in whole rounds (image layer 3 entry: +18 % there); the qkv GEMMs (Cout = 3 K) keep 256 x 256.
+  // grid fills the chip in whole rounds (image layer 3 entry: +18 % there), and the 1x1 stride-2 residual downsamples
+  // (tools/gpu_r6y.sh); the qkv GEMMs (Cout = 3 K) keep 256 x 256.
   if (M >= 16384 && a.prec == 0 && a.Cin % KC == 0 && a.Cout % 128 == 0) {
     const bool mlp = gemm && ((a.Cout >= 1024 && a.Cout % 1024 == 0 && K <= 512) || (K >= 1024 && a.Cout >= 256) ||
                               (a.Cout == K && K >= 512));
     const bool s2 = a.stride == 2 && a.KH == 3 && a.KW == 3 &&
                     !(a.Cout >= 256 && (m256 * n256) % 256 == 0);
-    if (mlp || s2) {
+    const bool ds = a.stride == 2 && a.KH == 1 && a.KW == 1;  // the residual downsamples: -6 to -24 %
+    if (mlp || s2 || ds) {
       launch_x5_cfg<4, 2, 1, 2, 2>(a, M, K, st);
       return true;
     }

@@ -92,6 +92,8 @@ def test_conv2d(gpu, B, H, W, Cin, Cout, k, s, p, relu, res):
     (1, 70, 130, 160, 400, 1, 1, 0, False, True), # 128 x 128 tiles, ragged M and N
     (1, 64, 128, 132, 512, 1, 1, 0, True, False), # 128 x 128 tiles, generic K (Cin % 32 != 0)
     (1, 256, 256, 64, 256, 3, 2, 1, True, False), # 128 x 128 tiles, 3x3 stride-2 tap walk
+    (4, 130, 126, 64, 128, 1, 2, 0, False, False),# 1x1 stride-2 downsample, 128 x 128 two per CU, ragged M
+    (1, 161, 128, 256, 1024, 1, 1, 0, True, False),# GPT MLP-up shape (C = 256), 128 x 128 two per CU, ragged M
     # 3x3 / stride 1 convs take the halo-reuse direct kernel (conv_x6.hip)
     (2, 8, 40, 128, 192, 3, 1, 1, True, True),    # 8 x 32 tiles, ragged W, BN 64 x 3
     (1, 12, 70, 64, 100, 3, 1, 1, False, True),   # 8 x 32 tiles ragged in H and W, ragged N
