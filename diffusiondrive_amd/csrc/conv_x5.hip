@@ -479,6 +479,13 @@ bool launch_conv_x5(const ConvArgs& a, int M, int K, hipStream_t st) {
   // GEMMs (C = 256 / 512: -4 to -21 %) and the C = 512 proj, and the stride-2 3x3 convs except where the 256 x 256
   // grid fills the chip in whole rounds (image layer 3 entry: +18 % there), and the 1x1 stride-2 residual downsamples
   // (tools/gpu_r6y.sh); the qkv GEMMs (Cout = 3 K) keep 256 x 256.
+  // bf16 (config C4's trunk mode): the short-K 1x1 GEMMs - the ResNet-50 bottleneck expands, HBM-bound on their
+  // outputs - on the same two-per-CU tiles (C4 forward -0.35 ms; the compute-heavy GEMMs and the strided downsamples
+  // lost there, tools/gpu_r6aa.sh, profiles/round6/x5_t128_ab.md)
+  if (M >= 16384 && a.prec == 1 && gemm && K <= 256 && a.Cin % KC == 0 && a.Cout % 128 == 0) {
+    launch_x5_cfg<4, 2, 1, 2, 2>(a, M, K, st);
+    return true;
+  }
   if (M >= 16384 && a.prec == 0 && a.Cin % KC == 0 && a.Cout % 128 == 0) {
     const bool mlp = gemm && ((a.Cout >= 1024 && a.Cout % 1024 == 0 && K <= 512) || (K >= 1024 && a.Cout >= 256) ||
                               (a.Cout == K && K >= 512));
