@@ -255,7 +255,7 @@ def test_conv_x3_k_split(gpu, monkeypatch, B, H, W, Cin, Cout, k, s):
     (4, 64, 256, 64, 64, 3, 1, 1, False, "conv_x6<16,16,64,4,2,bf16>"),     # layer1 (8-wave BN 64 form)
     (2, 12, 70, 128, 100, 3, 1, 1, True, "conv_x6<8,8,64,2,2,bf16>"),       # ragged H / W / N: a small grid, 8 x 8 tiles
     (1, 160, 128, 512, 2048, 1, 1, 0, False, "conv_x5<256,256,bf16>"),      # GPT MLP-up (M = 20480)
-    (64, 64, 256, 64, 256, 1, 1, 0, True, "conv_x5<256,256,bf16>"),         # ResNet-50 layer1 expand 1x1
+    (64, 64, 256, 64, 256, 1, 1, 0, True, "conv_x5<128,128,bf16>"),         # ResNet-50 layer1 expand 1x1 (2 WG / CU)
     (64, 64, 256, 64, 128, 3, 2, 1, False, "conv_x5<256,128,bf16>"),        # stage entry 3x3 / s2
     (16, 64, 64, 36, 64, 3, 1, 1, False, "conv_x5<256,64,bf16>"),           # generic K (Cin % 32 != 0)
     (3, 5, 7, 320, 40, 1, 1, 0, True, "conv_x3<64,64,bf16>"),               # small grid: register-staged kernel
