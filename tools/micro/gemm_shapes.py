@@ -7,7 +7,7 @@ import glob
 import os
 import sys
 
-SHAPES = [(1536, 512), (2048, 512), (512, 2048), (768, 256), (1024, 256), (512, 512), (256, 1024), (256, 256)]
+SHAPES = [(128, 512), (256, 256), (128, 128), (64, 256), (256, 64), (64, 64), (192, 64), (512, 128), (384, 128)]
 REPS = 13
 
 if "--parse" in sys.argv:
