@@ -1,4 +1,4 @@
-# round 6 (r): conv_x6 with the F0 MFMAs held ahead of the step barrier - conv_bench (the trunk's 3x3 shapes at B = 64,
+# round 6 (r): conv_x6 A/B against the previous build (tools/micro/ab/old/libddmi.so): conv_bench 3x3 shapes, alternating, then the bench
 # error vs the fp32 kernel) against the previous build (tools/micro/ab/old/libddmi.so), alternating, then the bench
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
