@@ -643,19 +643,24 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
       F.al[i] = *reinterpret_cast<const vp_h8*>(ubuf + (o ^ 32));
     }
   };
-  auto mfma_frag = [&](const Frag& F) {  // small terms first, the hi x hi term last
+  // small terms first, the hi x hi term last: the cross terms (part 0) go ahead of the next step's barrier, the
+  // hi x hi term (part 1) after it, under the next step's fragment reads
+  auto mfma_part = [&](const Frag& F, auto PART) {
+    if constexpr (decltype(PART)::value == 0) {
 #pragma unroll
-    for (int i = 0; i < VU_TM; ++i)
+      for (int i = 0; i < VU_TM; ++i)
 #pragma unroll
-      for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[i], F.bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[i], F.bh[j], acc[i][j], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < VU_TM; ++i)
+      for (int i = 0; i < VU_TM; ++i)
 #pragma unroll
-      for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bl[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bl[j], acc[i][j], 0, 0, 0);
+    } else {
 #pragma unroll
-    for (int i = 0; i < VU_TM; ++i)
+      for (int i = 0; i < VU_TM; ++i)
 #pragma unroll
-      for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < VU_TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+    }
   };
 
   // Barrier opening step (g, t): this wave's B(g, t) DMAs have landed (vmcnt = memory ops issued after them: B of
@@ -707,6 +712,8 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
     constexpr int t1 = (t + 1) % 9;
     const int g1 = t == 8 ? g + 1 : g;
     if (++slot == VU_NSLOT) slot = 0;
+    mfma_part(Fc, std::integral_constant<int, 0>());
+    __builtin_amdgcn_sched_barrier(0);
     // (t < 8: g1 = g < gend, known at compile time - a runtime test here would merge two paths before the MFMAs,
     // and the compiler's wait count at the merge would make them wait for the fragment reads issued just above)
     if (t != 8 || g1 < gend) {
@@ -715,7 +722,7 @@ __global__ __launch_bounds__(VU_NT, 1) void vproj_union_kernel(VprojArgs a) {
       load_frag(Fn, slot, g1, std::integral_constant<int, t1>());
     }
     __builtin_amdgcn_sched_barrier(0);
-    mfma_frag(Fc);
+    mfma_part(Fc, std::integral_constant<int, 1>());
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (t == VU_TS) {
       // the union of group g + 1 was issued when step TA opened; younger: B issued at the opens of taps TA+1 .. TS+1
